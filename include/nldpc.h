@@ -1,0 +1,138 @@
+/*
+ * nldpc.h — C ABI of the MI355X-native neural belief-propagation LDPC decoder.
+ *
+ * The reference (ShapeLayer/neural-ldpc-decoder-torch) has no FFI: its hot path is the Python
+ * nn.Module API.  This header is the native boundary that the drop-in modules
+ * (neural-ldpc-decoder-torch_amd/src/{neural_ldpc_decoder,boosted_neural_ldpc_decoder}) bind
+ * through ctypes; each entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *   - int status: 0 = NLDPC_OK; anything else is an error, nldpc_last_error() gives the text
+ *     (thread-local).  No C++ exception crosses this boundary.
+ *   - Every tensor argument is a DEVICE pointer to contiguous fp32 (or the stated type) memory,
+ *     allocated by the caller (e.g. the torch caching allocator).  Host arrays are marked "host".
+ *   - All launches are stream-ordered on the `stream` argument (a hipStream_t); no entry point
+ *     synchronises the device or allocates device memory, so every call is graph-capturable.
+ *   - A graph handle owns only its device edge tables; it is immutable after creation and may be
+ *     used from several streams at once.
+ *   - Layouts: channel LLR xa [B][N][Z]; outputs [B][N*Z] (bit index j*Z+v, reference layout);
+ *     message state [B][E][Z] with E in C-order (row-major over the base graph).
+ */
+#ifndef NLDPC_H
+#define NLDPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NLDPC_ABI_VERSION 1
+
+enum nldpc_status {
+    NLDPC_OK = 0,
+    NLDPC_EINVAL = 1,      /* bad argument (ValueError on the Python side) */
+    NLDPC_EHIP = 2,        /* HIP runtime error */
+    NLDPC_EUNSUPPORTED = 3 /* valid but not implemented configuration */
+};
+
+/* Decoder kinds.  SP/MS/QMS keep the reference DecoderType values
+ * (src/boosted_neural_ldpc_decoder/struct/DecoderType.py:4-7); NEURAL is
+ * src/neural_ldpc_decoder/NeuralLDPCDecoder.py. */
+enum nldpc_kind { NLDPC_SP = 0, NLDPC_MS = 1, NLDPC_QMS = 2, NLDPC_NEURAL = 3 };
+
+typedef struct nldpc_graph nldpc_graph;
+
+/* Per-call decoder configuration (the constructor arguments of BoostedNeuralLDPCDecoder,
+ * BoostedNeuralLDPCDecoder.py:15-49, reduced to what the arithmetic needs). */
+typedef struct nldpc_cfg {
+    int32_t kind;    /* enum nldpc_kind */
+    int32_t qbit;    /* QMS quantiser: 6, 5, -5, 4, 3; anything else = identity (:187-214) */
+    int32_t ucn;     /* 1: compute unsatisfied-check flags and mix w_ucn (:339-374, :436-488) */
+    int32_t vn_cumulative; /* 1: xin_t = Q(xin_{t-1} * w_vn[t]) (:325-337); 0: no VN weight */
+    float llr_lo;    /* allowed_llr_range.start (Clipping, :36) */
+    float llr_hi;    /* allowed_llr_range.end */
+    int32_t first_iter; /* absolute index of the first iteration of this call (UCN uses xin at 0) */
+    int32_t c2v_in;  /* 1: read the c2v state at the start; 0: start from all-zero messages */
+    int32_t vn_prefix; /* rows of w_vn applied before this call's first iteration (cumulative VN
+                          weighting carried over earlier iterations of the same forward) */
+    int32_t reserved;
+} nldpc_cfg;
+
+/* ---- library ---------------------------------------------------------------------------- */
+int nldpc_abi_version(void);
+const char* nldpc_last_error(void);
+
+/* ---- graph: replaces ConnectingMatrix(Z, basegraph) + ConnectingMatrixTorch(cm, device)
+ *      (src/boosted_neural_ldpc_decoder/ConnectingMatrix.py:5-80, ConnectingMatrixTorch.py:7-54;
+ *       src/neural_ldpc_decoder/ConnectingMatrix.py:4-66, ConnectingMatrixTorch.py:7-46).
+ *      basegraph: host [M*N] row-major shift table, -1 = no edge; shifts are taken mod Z. ------ */
+int nldpc_graph_create(int32_t M, int32_t N, int32_t Z, const int32_t* basegraph, int32_t device,
+                       nldpc_graph** out);
+int nldpc_graph_destroy(nldpc_graph* g);
+/* dims[0..7] = M, N, Z, E, max check degree, max variable degree, device, reserved */
+int nldpc_graph_dims(const nldpc_graph* g, int32_t* dims);
+/* host copies of the C-order edge tables: check, variable, shift (mod Z) of every edge */
+int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t* shift);
+
+/* ---- decode forward: replaces NeuralLDPCDecoder.forward (NeuralLDPCDecoder.py:44-100) and
+ *      BoostedNeuralLDPCDecoder.forward (BoostedNeuralLDPCDecoder.py:260-538).
+ *   T        iterations run by this call (iteration k of the call = absolute cfg->first_iter + k)
+ *   xa       [B][N][Z] channel LLRs
+ *   w_cn     [T][E] per-edge check-node weight, NULL = |x| (sharing code 0).  Shared codes (per
+ *            check, per iteration) are expanded to per-edge by the caller.
+ *   w_ucn    [T][E] per-edge UCN weight (cfg->ucn), else NULL
+ *   bias     [T][E] per-edge bias (NEURAL), else NULL
+ *   w_vn     [vn_prefix + T][N] per-column VN weights (cfg->vn_cumulative), else NULL; iteration k
+ *            of the call uses xin = Q(..Q(xa*w_vn[0])..*w_vn[vn_prefix+k])
+ *   outs     host array of T device pointers, each [B][N*Z]; NULL entries are not written
+ *            (with cfg->ucn every entry but the last must be non-NULL: iteration k reads k-1)
+ *   app_prev [B][N*Z] posterior of iteration first_iter-1 (UCN with first_iter > 0), else NULL
+ *   c2v      [B][E][Z] message state in/out: read at the start when cfg->c2v_in (otherwise a
+ *            fresh all-zero state), holds the state after the last iteration on return
+ *   v2c      [B][E][Z] scratch, or NULL when `saved` is given
+ *   saved    [T][B][E][Z] per-iteration variable-to-check messages kept for nldpc_backward,
+ *            or NULL (inference)
+ *   stream   hipStream_t */
+int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
+                  const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
+                  float* const* outs, const float* app_prev, float* c2v, float* v2c, float* saved,
+                  void* stream);
+
+/* ---- decode backward (config 5: training through the unrolled decoder; the reference gets this
+ *      from autograd over BoostedNeuralLDPCDecoder.py:320-526 / NeuralLDPCDecoder.py:54-98).
+ *   outs       forward outputs (needed for UCN flags and the output clamp mask)
+ *   grad_outs  host array of T device pointers [B][N*Z] (NULL entry = zero gradient)
+ *   saved      as written by nldpc_forward
+ *   g_w_cn, g_w_ucn, g_bias: [T][E] accumulated (+=) per-edge gradients, NULL if not wanted
+ *   g_w_vn     [T][N] accumulated (+=) per-column gradients, NULL if not wanted
+ *   work       device scratch of nldpc_backward_workspace() bytes */
+int nldpc_backward_workspace(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T,
+                             size_t* bytes);
+int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
+                   const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
+                   const float* const* outs, const float* const* grad_outs, const float* app_prev,
+                   const float* saved, float* g_w_cn, float* g_w_ucn, float* g_bias, float* g_w_vn,
+                   void* work, size_t work_bytes, void* stream);
+
+/* ---- BER/FER accounting: replaces Functions.evaluate_ber_fer (Functions.py:85-102) and the
+ *      per-iteration .item() loop of train/train_BoostedNeuralLDPCDecoder.py:363-383.
+ *   llr [B][L]; y [B][L] uint8 bits or NULL (all-zero codeword); counts int64[2] += (bit errors,
+ *   frame errors).  convention 0: bit = (LLR > 0) (decoder convention);
+ *   convention 1: bit = (LLR < 0) (the reference helper's literal, inverted rule). */
+int nldpc_ber_count(const float* llr, const uint8_t* y, int64_t B, int64_t L, int32_t convention,
+                    int64_t* counts, void* stream);
+
+/* ---- synthetic AWGN channel (the step before the path; replaces the all-zero branch of
+ *      AWGNPassedDatagen, boosted.../AWGNPassedDatagen.py:75-134, generated on the device):
+ *   xa[b][n] = 2*(-1 + sigma*g)/sigma^2 with g ~ N(0,1) from Philox-4x32-10(seed) at counter
+ *   (b_offset + b)*L + n, so a sharded run draws the same noise as a single-device run.
+ *   qbit != 0 applies the QMS quantiser (Functions.Cal_MSA_Q, Functions.py:69-83). */
+int nldpc_awgn_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,
+                   int32_t qbit, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NLDPC_H */

@@ -1,0 +1,116 @@
+// The steps either side of the decode path:
+//   nldpc_awgn_llr   synthetic BPSK/AWGN channel LLRs generated in HBM (Philox-4x32-10 + Box-Muller)
+//   nldpc_ber_count  fused bit/frame error counting of a posterior (Functions.evaluate_ber_fer)
+#include <hip/hip_runtime.h>
+
+#include "nldpc_internal.h"
+#include "nldpc_math.h"
+
+namespace nldpc {
+
+// ---------------------------------------------------------------- Philox-4x32-10 (Salmon et al. 2011)
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+    constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+        const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+
+__device__ __forceinline__ double u01(uint32_t r) { return ((double)r + 1.0) * (1.0 / 4294967296.0); }
+
+// one thread = 4 consecutive elements of the global (b_offset + b) * L + n stream
+__global__ __launch_bounds__(256) void awgn_kernel(float* xa, int64_t total, int64_t first, double sigma,
+                                                   uint64_t seed, int qbit) {
+    const int64_t g4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // local group of 4
+    const int64_t g0 = (first >> 2) + g4;                                 // global group index
+    const int64_t e0 = g0 * 4;
+    if (e0 >= first + total) return;
+    U4 r = philox4x32_10(U4{(uint32_t)g0, (uint32_t)(g0 >> 32), 0u, 0u}, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const double rad0 = sqrt(-2.0 * log(u01(r.x))), th0 = 6.283185307179586 * u01(r.y);
+    const double rad1 = sqrt(-2.0 * log(u01(r.z))), th1 = 6.283185307179586 * u01(r.w);
+    const double n[4] = {rad0 * cos(th0), rad0 * sin(th0), rad1 * cos(th1), rad1 * sin(th1)};
+    const double s2 = sigma * sigma;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t e = e0 + q;
+        if (e < first || e >= first + total) continue;
+        // all-zero codeword: BPSK bit 0 -> -1 (AWGNPassedDatagen.py:97-103), LLR = 2 y / sigma^2
+        float llr = (float)(2.0 * (-1.0 + sigma * n[q]) / s2);
+        if (qbit) llr = quantize(llr, qbit);
+        xa[e - first] = llr;
+    }
+}
+
+__global__ __launch_bounds__(256) void ber_kernel(const float* llr, const uint8_t* y, int64_t B, int64_t L,
+                                                  int convention, unsigned long long* counts) {
+    __shared__ unsigned long long s_bits[4];
+    __shared__ int s_frame[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long bits_acc = 0;
+    unsigned long long frames_acc = 0;
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        unsigned long long cnt = 0;
+        const float* row = llr + b * L;
+        const uint8_t* yr = y ? y + b * L : nullptr;
+        for (int64_t n = threadIdx.x; n < L; n += blockDim.x) {
+            const float x = row[n];
+            const int bit = convention == 0 ? (x > 0.f) : (x < 0.f);
+            const int ref = yr ? (yr[n] != 0) : 0;
+            cnt += (bit != ref);
+        }
+        // wave reduce (64 lanes)
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
+        if (lane == 0) s_bits[wid] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long t = 0;
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_bits[w];
+            bits_acc += t;
+            frames_acc += (t > 0);
+        }
+        __syncthreads();
+    }
+    (void)s_frame;
+    if (threadIdx.x == 0) {
+        atomicAdd(&counts[0], bits_acc);
+        atomicAdd(&counts[1], frames_acc);
+    }
+}
+
+}  // namespace nldpc
+
+using namespace nldpc;
+
+extern "C" int nldpc_awgn_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,
+                              int32_t qbit, void* stream) {
+    if (!xa || B <= 0 || L <= 0 || !(sigma > 0.f)) return fail(NLDPC_EINVAL, "nldpc_awgn_llr: bad argument");
+    const int64_t total = B * L;
+    const int64_t first = b_offset * L;
+    const int64_t groups = ((first + total + 3) >> 2) - (first >> 2);
+    const int64_t blocks = (groups + 255) / 256;
+    if (blocks > 0x7FFFFFFF) return fail(NLDPC_EUNSUPPORTED, "nldpc_awgn_llr: too large");
+    hipLaunchKernelGGL(awgn_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), xa, total,
+                       first, (double)sigma, seed, qbit);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NLDPC_OK : hip_fail(e, "awgn_kernel launch");
+}
+
+extern "C" int nldpc_ber_count(const float* llr, const uint8_t* y, int64_t B, int64_t L, int32_t convention,
+                               int64_t* counts, void* stream) {
+    if (!llr || !counts || B <= 0 || L <= 0) return fail(NLDPC_EINVAL, "nldpc_ber_count: bad argument");
+    const int64_t blocks = B < 4096 ? B : 4096;
+    hipLaunchKernelGGL(ber_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), llr, y, B, L,
+                       convention, reinterpret_cast<unsigned long long*>(counts));
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NLDPC_OK : hip_fail(e, "ber_kernel launch");
+}

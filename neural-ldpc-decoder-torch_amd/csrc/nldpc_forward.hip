@@ -1,0 +1,412 @@
+// Forward decode: the flooding belief-propagation iteration of the reference decoders as two
+// gather kernels per iteration over the lifted Tanner graph's edge list.
+//
+//   VN kernel  one thread per variable copy (b, j, v), lanes = consecutive v (coalesced):
+//              reads the column's c2v messages, writes every v2c message of the column
+//              (sum of the others, sequential fp32 in ascending check row) and, fused, the
+//              posterior output of the previous iteration (= the reference's W_output matmul +
+//              channel add of that iteration, NeuralLDPCDecoder.py:93-98 / Boosted…py:513-526).
+//   CN kernel  one thread per check copy (b, i, h), lanes = consecutive h: gathers the row's v2c
+//              at the cyclic shift (h + s_e) mod Z (the reference's lifting_matrix_1 GEMM), does
+//              the min-sum / sum-product update + learned weighting (NeuralLDPCDecoder.py:65-91,
+//              Boosted…py:386-512) and scatters c2v back to the same addresses (lifting_matrix_2).
+// Message state is [B][E][Z] fp32 in HBM with E in C-order; see DESIGN.md for the roofline.
+#include <hip/hip_runtime.h>
+
+#include "nldpc_internal.h"
+#include "nldpc_math.h"
+
+namespace nldpc {
+
+struct VNArgs {
+    DevGraph g;
+    int64_t B;
+    const float* xa;     // [B][N][Z]
+    const float* c2v;    // [B][E][Z] or nullptr (all-zero state)
+    float* v2c;          // [B][E][Z] or nullptr (posterior only)
+    float* post;         // [B][N][Z] or nullptr
+    const float* w_vn;   // [T][N] cumulative VN weights (boosted) or nullptr
+    int32_t n_vn_steps;  // number of cumulative weighting/quantisation steps for xin (k + 1)
+    int32_t qbit;
+    float lo, hi;
+};
+
+struct CNArgs {
+    DevGraph g;
+    int64_t B;
+    const float* v2c;    // [B][E][Z]
+    float* c2v;          // [B][E][Z]
+    const float* w_cn;   // [E] (this iteration) or nullptr
+    const float* w_ucn;  // [E] or nullptr
+    const float* bias;   // [E] or nullptr (Neural)
+    // UCN: hard-decision source.  app != nullptr: posterior [B][N][Z] of the previous iteration;
+    // else xin_0 recomputed from xa and w_vn0 (absolute iteration 0, Boosted…py:340-341).
+    const float* app;
+    const float* xa;
+    const float* w_vn0;  // [N] or nullptr
+    int32_t qbit;
+    float lo, hi;
+};
+
+// xin for the k-th iteration of a call: Q(...Q(Q(xa*w0)*w1)...) (Boosted…py:325-337).
+template <int KIND>
+__device__ __forceinline__ float vn_channel(float xa, const float* w_vn, int N, int j, int steps, int qbit) {
+    if (KIND == NLDPC_NEURAL) return xa;
+    float x = xa;
+    if (w_vn) {
+        for (int s = 0; s < steps; ++s) {
+            x = fmul(x, w_vn[(int64_t)s * N + j]);
+            if (KIND == NLDPC_QMS) x = quantize(x, qbit);
+        }
+    } else if (KIND == NLDPC_QMS) {
+        x = quantize(x, qbit);  // idempotent: Q applied every iteration equals Q applied once
+    }
+    return x;
+}
+
+template <int DV, int KIND>
+__global__ __launch_bounds__(256) void vn_kernel(VNArgs a) {
+    const int Z = a.g.Z, N = a.g.N, E = a.g.E;
+    const int64_t total = a.B * N * Z;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int v = (int)(idx % Z);
+    const int64_t bj = idx / Z;
+    const int j = (int)(bj % N);
+    const int64_t b = bj / N;
+    const int beg = a.g.col_ptr[j];
+    const int d = a.g.col_ptr[j + 1] - beg;
+    const float xav = a.xa[idx];
+    const int64_t base = b * E;
+
+    int eidx[DV];
+    float c[DV];
+#pragma unroll
+    for (int k = 0; k < DV; ++k) {
+        eidx[k] = k < d ? a.g.col_edge[beg + k] : 0;
+        c[k] = (k < d && a.c2v) ? a.c2v[(base + eidx[k]) * Z + v] : 0.f;
+    }
+
+    if (a.post) {
+        // y = ch_o + ((0 + c0) + c1 + ...)  (W_output sgemm order), Boosted: ch_o = Q(xa), clamp
+        float P = 0.f;
+#pragma unroll
+        for (int k = 0; k < DV; ++k)
+            if (k < d) P = fadd(P, c[k]);
+        float y;
+        if (KIND == NLDPC_NEURAL) {
+            y = fadd(xav, P);
+        } else {
+            const float xo = (KIND == NLDPC_QMS) ? quantize(xav, a.qbit) : xav;
+            y = clampf(fadd(xo, P), a.lo, a.hi);
+        }
+        a.post[idx] = y;
+    }
+
+    if (a.v2c) {
+        const float ch = vn_channel<KIND>(xav, a.w_vn, N, j, a.n_vn_steps, a.qbit);
+        const float x0 = fadd(0.f, ch);  // xa_input @ W_skipconn2even
+        float P = 0.f;                   // prefix ((0 + c0) + ... + c_{k-1})
+#pragma unroll
+        for (int k = 0; k < DV; ++k) {
+            if (k < d) {
+                float S = P;  // sum of the others, left to right, skipping k
+#pragma unroll
+                for (int m = k + 1; m < DV; ++m)
+                    if (m < d) S = fadd(S, c[m]);
+                a.v2c[(base + eidx[k]) * Z + v] = fadd(x0, S);
+                P = fadd(P, c[k]);
+            }
+        }
+    }
+}
+
+template <int DC, int KIND, bool UCN>
+__global__ __launch_bounds__(256) void cn_kernel(CNArgs a) {
+    const int Z = a.g.Z, M = a.g.M, E = a.g.E, N = a.g.N;
+    const int64_t total = a.B * M * Z;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int h = (int)(idx % Z);
+    const int64_t bi = idx / Z;
+    const int i = (int)(bi % M);
+    const int64_t b = bi / M;
+    const int beg = a.g.row_ptr[i];
+    const int d = a.g.row_ptr[i + 1] - beg;
+    const int64_t base = b * E;
+
+    int vv[DC];
+    float m[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k < d) {
+            int t = h + a.g.e_shift[beg + k];
+            vv[k] = t >= Z ? t - Z : t;
+            m[k] = a.v2c[(base + beg + k) * Z + vv[k]];
+        } else {
+            vv[k] = 0;
+            m[k] = 0.f;
+        }
+    }
+
+    // unsatisfied-check flag of (i, h): odd number of row variables with APP >= 0 (Boosted…py:346-359)
+    float u = 0.f;
+    if (UCN) {
+        int par = 0;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (k < d) {
+                const int j = a.g.e_var[beg + k];
+                const int64_t off = (b * N + j) * Z + vv[k];
+                float app;
+                if (a.app) {
+                    app = a.app[off];
+                } else {
+                    app = a.xa[off];
+                    if (a.w_vn0) app = fmul(app, a.w_vn0[j]);
+                    if (KIND == NLDPC_QMS) app = quantize(app, a.qbit);
+                }
+                par ^= (-app <= 0.f) ? 1 : 0;
+            }
+        }
+        u = par ? 1.f : 0.f;
+    }
+
+    float out0[DC];
+    if (KIND == NLDPC_SP) {
+        float tv[DC];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (k < d) {
+                const float x = clampf(m[k], a.lo, a.hi);
+                float t = tanhf(fmul(-0.5f, x));
+                tv[k] = fadd(t, (fabsf(t) > 0.f) ? 0.f : 1.f);
+            } else {
+                tv[k] = 1.f;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (k < d) {
+                float P = 1.f;
+#pragma unroll
+                for (int l = 0; l < DC; ++l)
+                    if (l < d && l != k) P = fmul(P, tv[l]);
+                P = clampf(P, -kSpClip, kSpClip);
+                out0[k] = fmul(-2.f, atanhf(P));
+            } else {
+                out0[k] = 0.f;
+            }
+        }
+    } else {
+        float min1 = kMaskMag, min2 = kMaskMag;
+        int idx1 = -1;
+        unsigned npos = 0;
+        unsigned posm = 0;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (k < d) {
+                float x = m[k];
+                if (KIND == NLDPC_QMS) x = quantize(x, a.qbit);
+                if (KIND == NLDPC_MS) x = clampf(x, a.lo, a.hi);
+                if (KIND != NLDPC_NEURAL) x = fadd(x, fmul(kZeroFix, (fabsf(x) > 0.f) ? 0.f : 1.f));
+                const float ax = fabsf(x);
+                const unsigned pos = x > 0.f;
+                npos ^= pos;
+                posm |= pos << k;
+                if (ax > 0.f) {  // exact zeros are masked out of the min (Neural only; Boosted has none)
+                    if (ax < min1) {
+                        min2 = min1;
+                        min1 = ax;
+                        idx1 = k;
+                    } else if (ax < min2) {
+                        min2 = ax;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (k < d) {
+                float mag = (k == idx1) ? min2 : min1;
+                if (KIND != NLDPC_NEURAL) mag = (mag > kZeroFix) ? mag : fadd(mag, -kZeroFix);
+                const float sgn = ((npos ^ (posm >> k)) & 1u) ? 1.f : -1.f;
+                out0[k] = fmul(mag, sgn);
+            } else {
+                out0[k] = 0.f;
+            }
+        }
+    }
+
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k < d) {
+            const int e = beg + k;
+            const float x = out0[k];
+            const float ax = fabsf(x);
+            float r;
+            if (KIND == NLDPC_NEURAL) {
+                float t = fadd(fmul(ax, a.w_cn[e]), a.bias[e]);  // two roundings (:89)
+                r = fmul(relu_mask(t), signf_t(x));
+            } else {
+                float x1;
+                if (!a.w_cn) {
+                    x1 = ax;
+                } else if (UCN && a.w_ucn) {
+                    const float x11 = fmul(ax, a.w_cn[e]);
+                    const float x12 = fmul(ax, a.w_ucn[e]);
+                    x1 = fadd(fmul(x11, fadd(-u, 1.f)), fmul(x12, u));
+                } else {
+                    x1 = fmul(ax, a.w_cn[e]);
+                }
+                float x2 = relu_mask(x1);
+                x2 = (KIND == NLDPC_QMS) ? quantize(x2, a.qbit) : clampf(x2, a.lo, a.hi);
+                r = fmul(x2, signf_t(x));
+            }
+            a.c2v[(base + e) * Z + vv[k]] = r;
+        }
+    }
+}
+
+template <int DV, int KIND>
+static hipError_t launch_vn(const VNArgs& a, hipStream_t s) {
+    const int64_t total = a.B * a.g.N * a.g.Z;
+    const int64_t blocks = (total + 255) / 256;
+    hipLaunchKernelGGL((vn_kernel<DV, KIND>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int DC, int KIND, bool UCN>
+static hipError_t launch_cn(const CNArgs& a, hipStream_t s) {
+    const int64_t total = a.B * a.g.M * a.g.Z;
+    const int64_t blocks = (total + 255) / 256;
+    hipLaunchKernelGGL((cn_kernel<DC, KIND, UCN>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int KIND>
+static hipError_t dispatch_vn(int dv, const VNArgs& a, hipStream_t s) {
+    switch (deg_bucket(dv)) {
+        case 8: return launch_vn<8, KIND>(a, s);
+        case 16: return launch_vn<16, KIND>(a, s);
+        case 32: return launch_vn<32, KIND>(a, s);
+        default: return launch_vn<64, KIND>(a, s);
+    }
+}
+
+hipError_t vn_launch(int kind, const VNArgs& a, hipStream_t s) {
+    switch (kind) {
+        case NLDPC_NEURAL: return dispatch_vn<NLDPC_NEURAL>(a.g.max_dv, a, s);
+        case NLDPC_SP: return dispatch_vn<NLDPC_SP>(a.g.max_dv, a, s);
+        case NLDPC_MS: return dispatch_vn<NLDPC_MS>(a.g.max_dv, a, s);
+        default: return dispatch_vn<NLDPC_QMS>(a.g.max_dv, a, s);
+    }
+}
+
+template <int KIND, bool UCN>
+static hipError_t dispatch_cn2(const CNArgs& a, hipStream_t s) {
+    switch (deg_bucket(a.g.max_dc)) {
+        case 8: return launch_cn<8, KIND, UCN>(a, s);
+        case 16: return launch_cn<16, KIND, UCN>(a, s);
+        case 32: return launch_cn<32, KIND, UCN>(a, s);
+        default: return hipErrorInvalidValue;  // d_c > 32 needs a wider sign mask
+    }
+}
+
+template <int KIND>
+static hipError_t dispatch_cn(bool ucn, const CNArgs& a, hipStream_t s) {
+    return ucn ? dispatch_cn2<KIND, true>(a, s) : dispatch_cn2<KIND, false>(a, s);
+}
+
+hipError_t cn_launch(int kind, bool ucn, const CNArgs& a, hipStream_t s) {
+    switch (kind) {
+        case NLDPC_NEURAL: return dispatch_cn2<NLDPC_NEURAL, false>(a, s);
+        case NLDPC_SP: return dispatch_cn<NLDPC_SP>(ucn, a, s);
+        case NLDPC_MS: return dispatch_cn<NLDPC_MS>(ucn, a, s);
+        default: return dispatch_cn<NLDPC_QMS>(ucn, a, s);
+    }
+}
+
+int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T) {
+    if (!g || !cfg) return fail(NLDPC_EINVAL, "null graph or cfg");
+    if (B <= 0 || T <= 0) return fail(NLDPC_EINVAL, "B and T must be positive");
+    if (cfg->kind < NLDPC_SP || cfg->kind > NLDPC_NEURAL) return fail(NLDPC_EINVAL, "unknown decoder kind");
+    if (g->dev.max_dc > 32) return fail(NLDPC_EUNSUPPORTED, "check degree above 32 is not supported");
+    if (cfg->kind == NLDPC_NEURAL && (cfg->ucn || cfg->vn_cumulative))
+        return fail(NLDPC_EINVAL, "the Neural decoder has no UCN / VN weighting");
+    const int64_t cells = B * (int64_t)g->dev.N * g->dev.Z;
+    const int64_t cells_c = B * (int64_t)g->dev.M * g->dev.Z;
+    if (cells > 0xFFFFFF00LL || cells_c > 0xFFFFFF00LL)
+        return fail(NLDPC_EUNSUPPORTED, "batch too large for one launch (split the batch)");
+    return NLDPC_OK;
+}
+
+}  // namespace nldpc
+
+using namespace nldpc;
+
+extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
+                             const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
+                             float* const* outs, const float* app_prev, float* c2v, float* v2c, float* saved,
+                             void* stream) {
+    int st = validate_cfg(g, cfg, B, T);
+    if (st) return st;
+    if (!xa || !c2v || !outs) return fail(NLDPC_EINVAL, "nldpc_forward: xa, c2v and outs are required");
+    if (!v2c && !saved) return fail(NLDPC_EINVAL, "nldpc_forward: need v2c scratch or saved buffer");
+    if (cfg->kind == NLDPC_NEURAL && (!w_cn || !bias))
+        return fail(NLDPC_EINVAL, "nldpc_forward: the Neural decoder needs w_cn and bias");
+    if (cfg->ucn) {
+        for (int k = 0; k + 1 < T; ++k)
+            if (!outs[k]) return fail(NLDPC_EINVAL, "nldpc_forward: UCN needs every intermediate output");
+        if (cfg->first_iter > 0 && !app_prev)
+            return fail(NLDPC_EINVAL, "nldpc_forward: UCN after iteration 0 needs app_prev");
+    }
+    if (cfg->vn_cumulative && !w_vn) return fail(NLDPC_EINVAL, "nldpc_forward: vn_cumulative needs w_vn");
+    if (cfg->vn_prefix < 0 || (cfg->vn_prefix > 0 && !cfg->vn_cumulative))
+        return fail(NLDPC_EINVAL, "nldpc_forward: vn_prefix needs vn_cumulative");
+    DeviceGuard guard(g->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const DevGraph& G = g->dev;
+    const int64_t EZ = (int64_t)G.E * G.Z;
+    bool state_valid = cfg->c2v_in != 0;
+    for (int k = 0; k < T; ++k) {
+        float* v2c_k = saved ? saved + (int64_t)k * B * EZ : v2c;
+        VNArgs va{G,
+                  B,
+                  xa,
+                  state_valid ? c2v : nullptr,
+                  v2c_k,
+                  k >= 1 ? outs[k - 1] : nullptr,
+                  cfg->vn_cumulative ? w_vn : nullptr,
+                  cfg->vn_prefix + k + 1,
+                  cfg->qbit,
+                  cfg->llr_lo,
+                  cfg->llr_hi};
+        hipError_t e = vn_launch(cfg->kind, va, s);
+        if (e != hipSuccess) return hip_fail(e, "vn_kernel launch");
+        const float* app = nullptr;
+        if (cfg->ucn) app = k >= 1 ? outs[k - 1] : (cfg->first_iter > 0 ? app_prev : nullptr);
+        CNArgs ca{G,
+                  B,
+                  v2c_k,
+                  c2v,
+                  w_cn ? w_cn + (int64_t)k * G.E : nullptr,
+                  (cfg->ucn && w_ucn) ? w_ucn + (int64_t)k * G.E : nullptr,
+                  bias ? bias + (int64_t)k * G.E : nullptr,
+                  app,
+                  xa,
+                  cfg->vn_cumulative ? w_vn : nullptr,
+                  cfg->qbit,
+                  cfg->llr_lo,
+                  cfg->llr_hi};
+        e = cn_launch(cfg->kind, cfg->ucn != 0, ca, s);
+        if (e != hipSuccess) return hip_fail(e, "cn_kernel launch");
+        state_valid = true;
+    }
+    if (outs[T - 1]) {
+        VNArgs va{G, B, xa, c2v, nullptr, outs[T - 1], nullptr, 0, cfg->qbit, cfg->llr_lo, cfg->llr_hi};
+        hipError_t e = vn_launch(cfg->kind, va, s);
+        if (e != hipSuccess) return hip_fail(e, "posterior launch");
+    }
+    return NLDPC_OK;
+}

@@ -1,0 +1,74 @@
+// Internal declarations shared by the translation units of libnldpc.so (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "nldpc.h"
+
+namespace nldpc {
+
+// Device edge tables of one lifted QC graph.  All arrays live in a single device allocation.
+//   e_chk/e_var/e_shift [E]  C-order edges (row-major over the base graph; ConnectingMatrix.py:92-99)
+//   row_ptr [M+1]            edges of check row i are the contiguous C-order range row_ptr[i]..
+//   col_ptr [N+1], col_edge  edges of column j in ascending check row (== ascending C-order index)
+struct DevGraph {
+    int32_t M, N, Z, E, max_dc, max_dv;
+    const int32_t* e_chk;
+    const int32_t* e_var;
+    const int32_t* e_shift;
+    const int32_t* row_ptr;
+    const int32_t* col_ptr;
+    const int32_t* col_edge;
+};
+
+}  // namespace nldpc
+
+struct nldpc_graph {
+    nldpc::DevGraph dev;
+    int32_t device;
+    void* blob;  // device allocation backing the tables
+    // host mirrors
+    int32_t* h_chk;
+    int32_t* h_var;
+    int32_t* h_shift;
+};
+
+namespace nldpc {
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+// RAII guard: make the graph's device current for the duration of a call, restore afterwards.
+struct DeviceGuard {
+    int prev = -1;
+    bool changed = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+            changed = hipSetDevice(dev) == hipSuccess;
+        }
+    }
+    ~DeviceGuard() {
+        if (changed) (void)hipSetDevice(prev);
+    }
+};
+
+// Pick the smallest compiled register-array bound that covers a degree.
+inline int deg_bucket(int d) {
+    if (d <= 8) return 8;
+    if (d <= 16) return 16;
+    if (d <= 32) return 32;
+    if (d <= 64) return 64;
+    return -1;
+}
+
+}  // namespace nldpc
+
+#define NLDPC_HIP_CHECK(expr)                                       \
+    do {                                                            \
+        hipError_t _e = (expr);                                     \
+        if (_e != hipSuccess) return ::nldpc::hip_fail(_e, #expr);  \
+    } while (0)

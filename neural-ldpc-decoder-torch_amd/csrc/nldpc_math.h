@@ -1,0 +1,71 @@
+// Device-side scalar arithmetic shared by the forward and backward kernels.
+//
+// Every helper reproduces one fp32 operation sequence of the reference exactly:
+// one IEEE rounding per reference op, no contraction (the library is built with
+// -ffp-contract=off and the products/sums below use explicit _rn intrinsics), round-half-even
+// quantisation, and the reference's masking constants.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace nldpc {
+
+__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+
+// torch.clamp(x, lo, hi): NaN passes through
+__device__ __forceinline__ float clampf(float x, float lo, float hi) {
+    float y = x < lo ? lo : x;
+    return y > hi ? hi : y;
+}
+
+// torch.sign
+__device__ __forceinline__ float signf_t(float x) { return (float)(x > 0.f) - (float)(x < 0.f); }
+
+// x * (x > 0).float()  (the reference's ReLU-by-mask, NeuralLDPCDecoder.py:90, Boosted…py:505)
+__device__ __forceinline__ float relu_mask(float x) { return fmul(x, x > 0.f ? 1.f : 0.f); }
+
+// QMS quantiser (BoostedNeuralLDPCDecoder.py:187-214): forward value of the straight-through
+// estimator, x_clipped + (q_value - x_clipped), evaluated in fp32 like the reference.
+struct QRange {
+    float lo, hi;
+    bool active;
+};
+
+__device__ __forceinline__ QRange q_range(int q) {
+    switch (q) {
+        case 6: return {-15.5f, 15.5f, true};
+        case 5: return {-7.5f, 7.5f, true};
+        case -5: return {-15.f, 15.f, true};
+        case 4: return {-7.f, 7.f, true};
+        case 3: return {-6.f, 6.f, true};
+        default: return {0.f, 0.f, false};
+    }
+}
+
+__device__ __forceinline__ float quantize(float x, int q) {
+    float qv;
+    switch (q) {
+        case 6: qv = clampf(rintf(x), -15.5f, 15.5f); break;
+        case 5: qv = clampf(fmul(rintf(fmul(x, 2.f)), 0.5f), -7.5f, 7.5f); break;
+        case -5: qv = clampf(rintf(x), -15.f, 15.f); break;
+        case 4: qv = clampf(rintf(x), -7.f, 7.f); break;
+        case 3: qv = clampf(fmul(rintf(fmul(x, 0.5f)), 2.f), -6.f, 6.f); break;
+        default: return x;
+    }
+    const QRange r = q_range(q);
+    const float xc = clampf(x, r.lo, r.hi);
+    return fadd(xc, __fsub_rn(qv, xc));
+}
+
+// STE / clamp gradient mask: 1 on the closed interval (torch.clamp backward), else 0
+__device__ __forceinline__ float in_range(float x, float lo, float hi) { return (x >= lo && x <= hi) ? 1.f : 0.f; }
+
+// Check-node magnitude cap for entries masked out of the tile (NeuralLDPCDecoder.py:74,
+// Boosted…py:411-414): the masked value 10000 takes part in the min.
+constexpr float kMaskMag = 10000.f;
+constexpr float kZeroFix = 1e-4f;  // 0.0001 as fp32 (Boosted…py:393, :416)
+// 1 - 1e-7 rounded to fp32 (Boosted…py:406-407)
+constexpr float kSpClip = 0.99999988079071044921875f;
+
+}  // namespace nldpc

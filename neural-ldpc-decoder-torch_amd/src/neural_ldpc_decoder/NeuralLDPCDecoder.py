@@ -1,0 +1,51 @@
+"""NeuralLDPCDecoder (Dai et al. 2021 neural min-sum) on MI355X.
+
+Reference: src/neural_ldpc_decoder/NeuralLDPCDecoder.py:6-100.  Same constructor, parameters
+(`weights_var.{t}` init 0.5, `biases_var.{t}` init 0, one [E] vector each per iteration, C-order
+edges) and forward contract: forward(xa [B, N, Z]) -> list of T posteriors [B, N*Z].  The iteration
+loop runs as HIP kernels through libnldpc.so (nldpc.decode); gradients flow to the weights and
+biases through nldpc_backward.  The reference's dense routing buffers (W_*, Lift_Matrix*) are not
+registered (22.9 GB each at z=384); their keys in an old state_dict are accepted and ignored.
+"""
+import torch
+import torch.nn as nn
+
+from nldpc.decode import KIND_NEURAL, DecodeCfg, decode_autograd
+
+from .ConnectingMatrixTorch import ConnectingMatrixTorch
+
+_DENSE_BUFFERS = ("W_odd2even", "W_skipconn2even", "W_even2odd", "W_output", "Lift_Matrix1", "Lift_Matrix2")
+
+
+class NeuralLDPCDecoder(nn.Module):
+    def __init__(self, iter_node_counts, batch_size, connecting_matrix: ConnectingMatrixTorch):
+        super().__init__()
+        self.iter_node_counts = iter_node_counts
+        self.batch_size = batch_size
+        self.conn_mat = connecting_matrix
+        self.N = self.conn_mat.N
+        self.M = self.conn_mat.M
+        self.Z = self.conn_mat.Z
+        self.sum_edge = self.conn_mat.sum_edge
+        self.neurons_per_odd_layer = self.conn_mat.neurons_per_odd_layer
+        self.neurons_per_even_layer = self.conn_mat.neurons_per_even_layer
+        E = int(self.sum_edge)
+        self.weights_var = nn.ParameterList(
+            [nn.Parameter(torch.full((E,), 0.5, dtype=torch.float32)) for _ in range(iter_node_counts)])
+        self.biases_var = nn.ParameterList(
+            [nn.Parameter(torch.zeros(E, dtype=torch.float32)) for _ in range(iter_node_counts)])
+        self._cfg = DecodeCfg(kind=KIND_NEURAL)
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        for k in _DENSE_BUFFERS:  # reference checkpoints carry the dense routing buffers
+            state_dict.pop(prefix + k, None)
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                                      error_msgs)
+
+    def forward(self, xa):
+        T = self.iter_node_counts
+        w = torch.stack(list(self.weights_var))
+        b = torch.stack(list(self.biases_var))
+        outs, _ = decode_autograd(self.conn_mat.graph, self._cfg, xa, T, w_cn=w, bias=b)
+        return outs

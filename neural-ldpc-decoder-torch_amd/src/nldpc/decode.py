@@ -1,0 +1,153 @@
+"""Host side of the decode path: buffers, C-ABI calls and the autograd Functions.
+
+`decode(...)` runs T flooding iterations of a decoder on the device through nldpc_forward
+(include/nldpc.h).  `NeuralDecodeFn` / `BoostedDecodeFn` wrap it in torch.autograd so that
+NeuralLDPCDecoder / BoostedNeuralLDPCDecoder keep the reference's training semantics
+(gradients of the learned weights through every iteration) via nldpc_backward.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .graph import LiftedGraph
+
+KIND_SP, KIND_MS, KIND_QMS, KIND_NEURAL = _lib.NLDPC_SP, _lib.NLDPC_MS, _lib.NLDPC_QMS, _lib.NLDPC_NEURAL
+
+
+@dataclass
+class DecodeCfg:
+    kind: int
+    qbit: int = 5
+    ucn: bool = False
+    vn_cumulative: bool = False
+    llr_lo: float = -20.0
+    llr_hi: float = 20.0
+    first_iter: int = 0
+    vn_prefix: int = 0
+
+    def c_struct(self, c2v_in: bool) -> _lib.NldpcCfg:
+        return _lib.NldpcCfg(self.kind, int(self.qbit), int(bool(self.ucn)), int(bool(self.vn_cumulative)),
+                             float(self.llr_lo), float(self.llr_hi), int(self.first_iter), int(bool(c2v_in)),
+                             int(self.vn_prefix), 0)
+
+
+def _require_device_tensor(x: torch.Tensor, name: str):
+    if not isinstance(x, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if x.device.type != "cuda":
+        raise RuntimeError(f"{name} is on '{x.device}': the MI355X decoder needs ROCm device tensors (no CPU path)")
+
+
+def _f32c(t):
+    return None if t is None else t.detach().to(torch.float32).contiguous()
+
+
+def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn=None, w_ucn=None, bias=None,
+           w_vn=None, c2v=None, app_prev=None, save=False, out_mask=None):
+    """Run T iterations.  xa [B, N, Z] fp32 device tensor.  Weights: [T, E] / [T, N] tensors or None.
+
+    Returns (outputs [T, B, N*Z], c2v state [B, E, Z], saved [T, B, E, Z] or None).
+    c2v: optional incoming state [B, E, Z] (None = all-zero messages)."""
+    _require_device_tensor(xa, "xa")
+    if xa.dim() != 3 or xa.shape[1] != graph.N or xa.shape[2] != graph.Z:
+        raise ValueError(f"xa must be [B, {graph.N}, {graph.Z}], got {tuple(xa.shape)}")
+    dev = xa.device
+    B = int(xa.shape[0])
+    xa_c = _f32c(xa)
+    E, N, Z = graph.E, graph.N, graph.Z
+    outs = torch.empty((T, B, N * Z), dtype=torch.float32, device=dev)
+    if c2v is None:
+        state = torch.empty((B, E, Z), dtype=torch.float32, device=dev)
+        c2v_in = False
+    else:
+        state = c2v.detach().to(torch.float32).contiguous().clone()
+        c2v_in = True
+    saved = torch.empty((T, B, E, Z), dtype=torch.float32, device=dev) if save else None
+    scratch = None if save else torch.empty((B, E, Z), dtype=torch.float32, device=dev)
+    tensors = [None if (out_mask is not None and not out_mask[t]) else outs[t] for t in range(T)]
+    pp, keep = _lib.ptr_array(tensors)
+    w_cn, w_ucn, bias, w_vn = _f32c(w_cn), _f32c(w_ucn), _f32c(bias), _f32c(w_vn)
+    app = _f32c(app_prev)
+    c = cfg.c_struct(c2v_in)
+    L = _lib.lib()
+    st = L.nldpc_forward(graph.handle(dev), ctypes.byref(c), B, T, _lib.ptr(xa_c), _lib.ptr(w_cn), _lib.ptr(w_ucn),
+                         _lib.ptr(bias), _lib.ptr(w_vn), pp, _lib.ptr(app), _lib.ptr(state), _lib.ptr(scratch),
+                         _lib.ptr(saved), _lib.stream_of(dev))
+    del keep
+    _lib.check(st, "nldpc_forward")
+    return outs, state, saved
+
+
+def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, saved, *, w_cn=None, w_ucn=None,
+                    bias=None, w_vn=None, app_prev=None, need=(True, True, True, True)):
+    """Gradients of the per-edge / per-column weights.  Returns (g_w_cn, g_w_ucn, g_bias, g_w_vn)."""
+    dev = xa.device
+    B = int(xa.shape[0])
+    E, N = graph.E, graph.N
+    z = lambda shape, on: torch.zeros(shape, dtype=torch.float32, device=dev) if on else None  # noqa: E731
+    g_cn = z((T, E), w_cn is not None and need[0])
+    g_ucn = z((T, E), w_ucn is not None and need[1])
+    g_b = z((T, E), bias is not None and need[2])
+    g_vn = z((T, N), w_vn is not None and need[3])
+    c = cfg.c_struct(False)
+    L = _lib.lib()
+    h = graph.handle(dev)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(L.nldpc_backward_workspace(h, ctypes.byref(c), B, T, ctypes.byref(nbytes)), "nldpc_backward_workspace")
+    work = torch.empty((max(int(nbytes.value), 1),), dtype=torch.uint8, device=dev)
+    go = [None if g is None else g.to(torch.float32).contiguous() for g in grad_outs]
+    ob = [o for o in outs]
+    pg, keep1 = _lib.ptr_array(go)
+    po, keep2 = _lib.ptr_array(ob)
+    xa_c = _f32c(xa)
+    w_cn, w_ucn, bias, w_vn = _f32c(w_cn), _f32c(w_ucn), _f32c(bias), _f32c(w_vn)
+    st = L.nldpc_backward(h, ctypes.byref(c), B, T, _lib.ptr(xa_c), _lib.ptr(w_cn), _lib.ptr(w_ucn), _lib.ptr(bias),
+                          _lib.ptr(w_vn), po, pg, _lib.ptr(_f32c(app_prev)), _lib.ptr(saved), _lib.ptr(g_cn),
+                          _lib.ptr(g_ucn), _lib.ptr(g_b), _lib.ptr(g_vn), _lib.ptr(work), int(work.numel()),
+                          _lib.stream_of(dev))
+    del keep1, keep2
+    _lib.check(st, "nldpc_backward")
+    return g_cn, g_ucn, g_b, g_vn
+
+
+class DecodeFn(torch.autograd.Function):
+    """outputs = decoder(xa; w_cn, w_ucn, bias, w_vn) with gradients for the four weight tensors.
+
+    forward returns the T outputs as separate tensors (views of one [T, B, N*Z] buffer) plus the
+    final message state (non-differentiable)."""
+
+    @staticmethod
+    def forward(ctx, graph, cfg, T, c2v_in, app_prev, xa, w_cn, w_ucn, bias, w_vn):
+        need_grad = any(t is not None and t.requires_grad for t in (w_cn, w_ucn, bias, w_vn))
+        outs, state, saved = decode(graph, cfg, xa, T, w_cn=w_cn, w_ucn=w_ucn, bias=bias, w_vn=w_vn, c2v=c2v_in,
+                                    app_prev=app_prev, save=need_grad)
+        ctx.graph, ctx.cfg, ctx.T = graph, cfg, T
+        ctx.has_state_in = c2v_in is not None
+        ctx.set_materialize_grads(False)
+        if need_grad:
+            ctx.save_for_backward(xa, w_cn, w_ucn, bias, w_vn, app_prev, outs, saved)
+        ctx.mark_non_differentiable(state)
+        return (*outs.unbind(0), state)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        xa, w_cn, w_ucn, bias, w_vn, app_prev, outs, saved = ctx.saved_tensors
+        if ctx.has_state_in:
+            raise NotImplementedError("backward through a decode that resumed from a stored message state")
+        grad_outs = list(grads[:ctx.T])
+        need = (ctx.needs_input_grad[6], ctx.needs_input_grad[7], ctx.needs_input_grad[8], ctx.needs_input_grad[9])
+        g_cn, g_ucn, g_b, g_vn = decode_backward(ctx.graph, ctx.cfg, xa, ctx.T, grad_outs, outs.unbind(0), saved,
+                                                 w_cn=w_cn, w_ucn=w_ucn, bias=bias, w_vn=w_vn, app_prev=app_prev,
+                                                 need=need)
+        return (None, None, None, None, None, None, g_cn if need[0] else None, g_ucn if need[1] else None,
+                g_b if need[2] else None, g_vn if need[3] else None)
+
+
+def decode_autograd(graph, cfg, xa, T, *, w_cn=None, w_ucn=None, bias=None, w_vn=None, c2v=None, app_prev=None):
+    """Differentiable decode.  Returns (list of T outputs [B, N*Z], final state [B, E, Z])."""
+    res = DecodeFn.apply(graph, cfg, T, c2v, app_prev, xa, w_cn, w_ucn, bias, w_vn)
+    return list(res[:T]), res[T]

@@ -1,0 +1,119 @@
+"""GPU parity of the forward decode (HIP kernels through the C ABI) against the reference's golden
+outputs and the CPU oracle.  Neural / MS / QMS: bit-exact soft outputs; SP: hard decisions exact,
+soft values within rtol 1e-3 / atol 5e-3 (torch.prod order + device tanh/atanh ulps).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+BG2 = np.loadtxt(os.path.join(ROOT, "resources", "basegraph2_set0.txt"), int, delimiter="\t")
+WIMAX = np.loadtxt(os.path.join(ROOT, "resources", "wman_N0576_R34_z24.txt"), int, delimiter="\t")
+DEV = torch.device("cuda")
+
+
+def _bg(name):
+    return WIMAX if "wimax" in name else BG2
+
+
+def _graph(bg, Z):
+    from nldpc.graph import LiftedGraph
+    return LiftedGraph(bg, Z)
+
+
+def expand_cn(g, w, code):
+    w = torch.as_tensor(w, dtype=torch.float32, device=DEV)
+    if code in (1, 4):
+        return w
+    if code == 2:
+        return w[torch.as_tensor(g.chk, device=DEV)]
+    return w.reshape(-1)[:1].expand(g.E)
+
+
+def expand_vn(g, w, code):
+    w = torch.as_tensor(w, dtype=torch.float32, device=DEV)
+    return w if code == 2 else w.reshape(-1)[:1].expand(g.N)
+
+
+def boosted_params(d, g, T, nw, fixed):
+    cn, ucn, vn = nw
+
+    def fetch(node, code, t):
+        if code in (1, 2, 3):
+            k = t
+        elif fixed:
+            v = [i for i in fixed if i <= t]
+            k = max(v) if v else fixed[0]
+        else:
+            k = 0
+        return d[f"param__weight_{node}_{k}"]
+
+    w_cn = torch.stack([expand_cn(g, fetch("CN", cn, t), cn) for t in range(T)]) if cn else None
+    use_ucn = ucn == cn and cn in (1, 2, 3)
+    w_ucn = torch.stack([expand_cn(g, fetch("UCN", ucn, t), ucn) for t in range(T)]) if use_ucn else None
+    w_vn = torch.stack([expand_vn(g, fetch("VN", vn, t), vn) for t in range(T)]) if vn in (2, 3) else None
+    return w_cn, w_ucn, w_vn, use_ucn
+
+
+@pytest.mark.parametrize("name", ["neural_cfg1_snr1_default", "neural_cfg1_snr2_default", "neural_cfg1_snr3_default",
+                                  "neural_cfg1_snr4_default", "neural_cfg1_snr2_random",
+                                  "neural_bg2_z16_b16_t5_random", "neural_wimax_z24_b16_t20_random"])
+def test_neural_forward_matches_reference(golden, name):
+    from nldpc.decode import KIND_NEURAL, DecodeCfg, decode
+    d = golden(name)
+    g = _graph(_bg(name), int(d["Z"]))
+    T = int(d["T"])
+    x = torch.from_numpy(d["x"]).to(DEV)
+    outs, _, _ = decode(g, DecodeCfg(KIND_NEURAL), x, T, w_cn=torch.from_numpy(d["weights"]).to(DEV),
+                        bias=torch.from_numpy(d["biases"]).to(DEV))
+    o = outs.cpu().numpy()
+    assert np.array_equal(o, d["outputs"]), f"{(o != d['outputs']).sum()} of {o.size} soft values differ"
+
+
+BOOSTED = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "boosted_*.npz")))
+
+
+@pytest.mark.parametrize("name", BOOSTED)
+def test_boosted_forward_matches_reference(golden, name):
+    from nldpc.decode import DecodeCfg, decode
+    d = golden(name)
+    g = _graph(_bg(name), int(d["Z"]))
+    T = 6 if "target6" in name else int(d["T"])
+    nw = tuple(int(v) for v in d["nw"])
+    fixed = [int(v) for v in d.get("fixed_nodes", [])]
+    w_cn, w_ucn, w_vn, use_ucn = boosted_params(d, g, T, nw, fixed)
+    kind, q = int(d["dtype"]), int(d["q"])
+    cfg = DecodeCfg(kind=kind, qbit=q, ucn=use_ucn, vn_cumulative=w_vn is not None)
+    x = torch.from_numpy(d["x"]).to(DEV)
+    outs, _, _ = decode(g, cfg, x, T, w_cn=w_cn, w_ucn=w_ucn, w_vn=w_vn)
+    o = outs.cpu().numpy()
+    ref = d["outputs"][:T]
+    assert np.array_equal(o > 0, ref > 0)
+    if kind == 0:
+        np.testing.assert_allclose(o, ref, rtol=1e-3, atol=5e-3)
+    else:
+        assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} soft values differ"
+
+
+@pytest.mark.parametrize("B", [1, 3, 8])
+def test_neural_z384_matches_oracle(B):
+    """BG2 z=384 (the headline graph; the reference cannot run it): GPU == CPU oracle bit for bit."""
+    from nldpc.decode import KIND_NEURAL, DecodeCfg, decode
+    from oracle.ldpc_oracle import OracleGraph, neural_forward
+    T = 4
+    g = _graph(BG2, 384)
+    gen = torch.Generator().manual_seed(B)
+    sigma = (1.0 / (2 * 0.2 * 10 ** 0.2)) ** 0.5
+    x = (2 * (-1 + sigma * torch.randn(B, 52, 384, generator=gen)) / sigma ** 2).float()
+    w = torch.rand(T, g.E, generator=gen) * 1.2
+    b = torch.randn(T, g.E, generator=gen) * 0.1
+    outs, _, _ = decode(g, DecodeCfg(KIND_NEURAL), x.to(DEV), T, w_cn=w.to(DEV), bias=b.to(DEV))
+    ref = torch.stack(neural_forward(OracleGraph(BG2, 384), x, list(w), list(b))).numpy()
+    o = outs.cpu().numpy()
+    assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} differ"
