@@ -1,0 +1,234 @@
+"""Benchmark: Neural BP decoding of 5G-NR BG2 z=384 at 20 iterations (BASELINE.json configs[2]/[3]).
+
+    python bench.py [--gpus N --steps K --warmup W]            # N=1: one process
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
+
+A step = one NeuralLDPCDecoder.forward over the rank's batch of B codewords (default 65536 per GPU,
+weak scaling), T=20 iterations, every iteration's posterior written (the reference API's output list).
+Inputs: synthetic all-zero codewords over BPSK/AWGN at Eb/N0 = 2 dB generated on the device
+(Philox, counter = global codeword index, so N GPUs decode exactly the codewords a single GPU would
+decode at B*N).  Timed region: barrier + synchronize on both sides of K steps, max over ranks.
+After timing: BER/FER of the last iteration summed over ranks with one RCCL all_reduce; on rank 0 at
+N=1 the CPU oracle (oracle/ldpc_oracle.py, the restatement pinned to the reference) is timed on a
+bounded sample of the same workload as the CPU baseline.
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "neural-ldpc-decoder-torch_amd", "src"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, Chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=65536, help="codewords per GPU")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--z", type=int, default=384)
+    ap.add_argument("--ebn0", type=float, default=2.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel timing")
+    return ap.parse_args()
+
+
+def kernel_bytes(B, E, N, Z, T):
+    """Algorithmic HBM bytes per launch kind: fp32 messages streamed once."""
+    f = 4
+    vn_first = B * f * (E * Z + N * Z)            # read xa, write v2c (all-zero state: no c2v read)
+    vn = B * f * (2 * E * Z + 2 * N * Z)          # read c2v + xa, write v2c + previous posterior
+    cn = B * f * (2 * E * Z)                      # gather v2c, scatter c2v
+    post = B * f * (E * Z + 2 * N * Z)            # read c2v + xa, write the last posterior
+    return {"vn": vn_first + (T - 1) * vn, "cn": T * cn, "post": post}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import neural_ldpc_decoder as nd
+    from nldpc import _lib
+    from nldpc.channel import ber_counts, sigma_for, awgn_llr
+
+    bg = np.loadtxt(os.path.join(ROOT, "resources", "basegraph2_set0.txt"), int, delimiter="\t")
+    M, N = bg.shape
+    Z, T, B = args.z, args.iters, args.batch
+    conn = nd.ConnectingMatrixTorch(nd.ConnectingMatrix(Z, bg), device=dev)
+    model = nd.NeuralLDPCDecoder(T, B, conn).to(dev)  # reference default parameters: w = 0.5, b = 0
+    E = int(conn.sum_edge)
+    rate = (N - M) / (N - 2)  # reference code-rate formula (AWGNPassedDatagen.py:47 / neural :36) = 0.2
+    sigma = sigma_for(args.ebn0, rate)
+    xa = awgn_llr(B, N, Z, sigma, seed=2042, b_offset=rank * B, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def barrier():
+        if dist:
+            tdist.barrier(device_ids=[local])
+
+    outs = None
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            outs = None
+            outs = model(xa)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        L = _lib.lib()
+        launches = args.steps * (2 * T + 1)
+        if not args.no_profile:
+            _lib.check(L.nldpc_profile_begin(launches), "nldpc_profile_begin")
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            outs = None
+            outs = model(xa)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        prof = None
+        if not args.no_profile:
+            import ctypes
+            ms = (ctypes.c_float * 3)()
+            cnt = (ctypes.c_int32 * 3)()
+            _lib.check(L.nldpc_profile_end(3, ms, cnt), "nldpc_profile_end")
+            prof = {"vn": (ms[0], cnt[0]), "cn": (ms[1], cnt[1]), "post": (ms[2], cnt[2])}
+
+        # BER / FER of every iteration on this rank's codewords (decoder convention bit = LLR > 0)
+        counts = ber_counts(outs)
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        tdist.all_reduce(t_max, op=tdist.ReduceOp.MAX)
+        tdist.all_reduce(counts, op=tdist.ReduceOp.SUM)  # the one RCCL exchange: BER accounting
+    elapsed = float(t_max.item())
+    counts = counts.cpu().numpy()
+
+    result = None
+    if rank == 0:
+        value = world * B * args.steps / elapsed
+        bits_total = world * B * N * Z
+        res = {
+            "metric": "codewords/sec + BER@Eb/N0, 5G-NR BG2 z=384, 20 iters, 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "codewords/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic: all-zero codewords, BPSK/AWGN Eb/N0={args.ebn0} dB, on-device Philox; "
+                    "reference default weights (w=0.5, b=0)",
+            "config": {"workload": f"cfg3 Neural BG2 set0 z={Z}, T={T}, all T posteriors written", "model": "NeuralLDPCDecoder",
+                       "global_batch": world * B, "per_gpu_batch": B, "seq_len": N * Z, "iters": T,
+                       "parallelism": f"dp{world}"},
+            "ber": {"ebn0_db": args.ebn0, "ber_last_iter": float(counts[-1, 0]) / bits_total,
+                    "fer_last_iter": float(counts[-1, 1]) / (world * B),
+                    "bit_errors_last_iter": int(counts[-1, 0]), "bits": bits_total,
+                    "ber_per_iter": [float(c) / bits_total for c in counts[:, 0]]},
+        }
+        if prof is not None:
+            kb = kernel_bytes(B, E, N, Z, T)
+            per = {}
+            for k in ("vn", "cn", "post"):
+                ms_tot, n = prof[k]
+                if n:
+                    byts = kb[k] * args.steps
+                    per[k] = {"avg_ms": ms_tot / n, "launches": n, "gbs": byts / (ms_tot / 1000.0) / 1e9,
+                              "alg_bytes_per_launch": byts / n}
+            dom = max(("vn", "cn"), key=lambda k: prof[k][0])
+            d = per[dom]
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                try:
+                    pj = json.load(open(pmc))
+                    key = f"{dom}_B{B}_Z{Z}"
+                    traffic = pj.get(key)
+                except Exception:
+                    traffic = None
+            res["roofline"] = {"bound": "hbm", "kernel": {"vn": "vn_kernel", "cn": "cn_kernel"}[dom],
+                               "achieved": round(d["gbs"], 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                               "frac": round(d["gbs"] / PEAK_HBM_GBS, 4), "traffic": traffic,
+                               "alg_bytes_per_launch": d["alg_bytes_per_launch"], "avg_launch_ms": round(d["avg_ms"], 4),
+                               "per_kernel": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
+                                                  for kk, vv in v.items()} for k, v in per.items()},
+                               "decode_equiv_gbs_survey_formula": round(
+                                   4 * (2 * T * E * Z + (T + 1) * N * Z) * world * B * args.steps / elapsed / 1e9, 1)}
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(bg, Z, T, sigma, args.cpu_seconds)
+        result = res
+        print(json.dumps(result), flush=True)
+    if dist:
+        tdist.barrier(device_ids=[local])
+        tdist.destroy_process_group()
+    return result
+
+
+def cpu_baseline(bg, Z, T, sigma, target_s):
+    """Time the CPU oracle (edge-list restatement of NeuralLDPCDecoder.forward, pinned bit-exact to the
+    reference) on a bounded sample of the same workload, on this host's cores."""
+    from oracle.ldpc_oracle import OracleGraph, neural_forward
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    cores = min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)))
+    torch.set_num_threads(cores)
+    g = OracleGraph(bg, Z)
+    E = g.E
+
+    def run(b):
+        gen = torch.Generator().manual_seed(7)
+        x = (2.0 * (-1.0 + sigma * torch.randn(b, g.N, Z, generator=gen, dtype=torch.float64)) / sigma ** 2).float()
+        w = [torch.full((E,), 0.5) for _ in range(T)]
+        bb = [torch.zeros(E) for _ in range(T)]
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            neural_forward(g, x, w, bb)
+        return time.perf_counter() - t0
+
+    b = 2
+    t = run(b)
+    b2 = int(max(2, min(512, b * target_s / max(t, 1e-3))))
+    if b2 > b:
+        b, t = b2, run(b2)
+    cpu_name = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(b / t, 3), "unit": "codewords/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/ldpc_oracle.py neural_forward, BG2 z={Z}, T={T}, B={b} codewords, "
+                      f"{t:.1f} s, torch {torch.__version__} CPU, {cpu_name}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -64,16 +64,34 @@ __device__ __forceinline__ float vn_channel(float xa, const float* w_vn, int N, 
     return x;
 }
 
+// Launch geometry shared by both kernels: blockDim = (Vt copies, Bt codewords); grid =
+// (ceil(B/Bt), nodes, ceil(Z/Vt)).  The node index (column j / check row i) is blockIdx.y, so a
+// workgroup works on one node and every graph-table load is wave-uniform (scalar); lanes run
+// along consecutive lifted copies v / h, so each wave touches 64 consecutive floats of a message row.
+struct Geo {
+    int v;      // lifted copy
+    int node;   // column j (VN) or check row i (CN)
+    int64_t b;  // codeword
+    bool ok;
+};
+
+__device__ __forceinline__ Geo geo(int64_t B, int Z) {
+    Geo g;
+    g.v = blockIdx.z * blockDim.x + threadIdx.x;
+    g.node = blockIdx.y;
+    g.b = (int64_t)blockIdx.x * blockDim.y + threadIdx.y;
+    g.ok = g.v < Z && g.b < B;
+    return g;
+}
+
 template <int DV, int KIND>
-__global__ __launch_bounds__(256) void vn_kernel(VNArgs a) {
+__global__ __launch_bounds__(512) void vn_kernel(VNArgs a) {
     const int Z = a.g.Z, N = a.g.N, E = a.g.E;
-    const int64_t total = a.B * N * Z;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= total) return;
-    const int v = (int)(idx % Z);
-    const int64_t bj = idx / Z;
-    const int j = (int)(bj % N);
-    const int64_t b = bj / N;
+    const Geo q = geo(a.B, Z);
+    if (!q.ok) return;
+    const int v = q.v, j = q.node;
+    const int64_t b = q.b;
+    const int64_t idx = (b * N + j) * Z + v;
     const int beg = a.g.col_ptr[j];
     const int d = a.g.col_ptr[j + 1] - beg;
     const float xav = a.xa[idx];
@@ -122,15 +140,12 @@ __global__ __launch_bounds__(256) void vn_kernel(VNArgs a) {
 }
 
 template <int DC, int KIND, bool UCN>
-__global__ __launch_bounds__(256) void cn_kernel(CNArgs a) {
-    const int Z = a.g.Z, M = a.g.M, E = a.g.E, N = a.g.N;
-    const int64_t total = a.B * M * Z;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= total) return;
-    const int h = (int)(idx % Z);
-    const int64_t bi = idx / Z;
-    const int i = (int)(bi % M);
-    const int64_t b = bi / M;
+__global__ __launch_bounds__(512) void cn_kernel(CNArgs a) {
+    const int Z = a.g.Z, E = a.g.E, N = a.g.N;
+    const Geo q = geo(a.B, Z);
+    if (!q.ok) return;
+    const int h = q.v, i = q.node;
+    const int64_t b = q.b;
     const int beg = a.g.row_ptr[i];
     const int d = a.g.row_ptr[i + 1] - beg;
     const int64_t base = b * E;
@@ -268,19 +283,27 @@ __global__ __launch_bounds__(256) void cn_kernel(CNArgs a) {
     }
 }
 
+static void geometry(int64_t B, int Z, int nodes, dim3& grid, dim3& block) {
+    const int vt = Z <= 512 ? Z : 256;
+    int bt = 256 / vt;
+    if (bt < 1) bt = 1;
+    block = dim3(vt, bt, 1);
+    grid = dim3((unsigned)((B + bt - 1) / bt), (unsigned)nodes, (unsigned)((Z + vt - 1) / vt));
+}
+
 template <int DV, int KIND>
 static hipError_t launch_vn(const VNArgs& a, hipStream_t s) {
-    const int64_t total = a.B * a.g.N * a.g.Z;
-    const int64_t blocks = (total + 255) / 256;
-    hipLaunchKernelGGL((vn_kernel<DV, KIND>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    dim3 grid, block;
+    geometry(a.B, a.g.Z, a.g.N, grid, block);
+    hipLaunchKernelGGL((vn_kernel<DV, KIND>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
 template <int DC, int KIND, bool UCN>
 static hipError_t launch_cn(const CNArgs& a, hipStream_t s) {
-    const int64_t total = a.B * a.g.M * a.g.Z;
-    const int64_t blocks = (total + 255) / 256;
-    hipLaunchKernelGGL((cn_kernel<DC, KIND, UCN>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    dim3 grid, block;
+    geometry(a.B, a.g.Z, a.g.M, grid, block);
+    hipLaunchKernelGGL((cn_kernel<DC, KIND, UCN>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
@@ -334,10 +357,7 @@ int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t 
     if (g->dev.max_dc > 32) return fail(NLDPC_EUNSUPPORTED, "check degree above 32 is not supported");
     if (cfg->kind == NLDPC_NEURAL && (cfg->ucn || cfg->vn_cumulative))
         return fail(NLDPC_EINVAL, "the Neural decoder has no UCN / VN weighting");
-    const int64_t cells = B * (int64_t)g->dev.N * g->dev.Z;
-    const int64_t cells_c = B * (int64_t)g->dev.M * g->dev.Z;
-    if (cells > 0xFFFFFF00LL || cells_c > 0xFFFFFF00LL)
-        return fail(NLDPC_EUNSUPPORTED, "batch too large for one launch (split the batch)");
+    if (B > 0x7FFFFFFFLL) return fail(NLDPC_EUNSUPPORTED, "batch too large for one launch (split the batch)");
     return NLDPC_OK;
 }
 
@@ -382,7 +402,9 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
                   cfg->qbit,
                   cfg->llr_lo,
                   cfg->llr_hi};
+        prof_start(PROF_VN, s);
         hipError_t e = vn_launch(cfg->kind, va, s);
+        prof_stop(s);
         if (e != hipSuccess) return hip_fail(e, "vn_kernel launch");
         const float* app = nullptr;
         if (cfg->ucn) app = k >= 1 ? outs[k - 1] : (cfg->first_iter > 0 ? app_prev : nullptr);
@@ -399,13 +421,17 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
                   cfg->qbit,
                   cfg->llr_lo,
                   cfg->llr_hi};
+        prof_start(PROF_CN, s);
         e = cn_launch(cfg->kind, cfg->ucn != 0, ca, s);
+        prof_stop(s);
         if (e != hipSuccess) return hip_fail(e, "cn_kernel launch");
         state_valid = true;
     }
     if (outs[T - 1]) {
         VNArgs va{G, B, xa, c2v, nullptr, outs[T - 1], nullptr, 0, cfg->qbit, cfg->llr_lo, cfg->llr_hi};
+        prof_start(PROF_POST, s);
         hipError_t e = vn_launch(cfg->kind, va, s);
+        prof_stop(s);
         if (e != hipSuccess) return hip_fail(e, "posterior launch");
     }
     return NLDPC_OK;

@@ -56,6 +56,12 @@ struct DeviceGuard {
     }
 };
 
+// benchmark instrumentation (nldpc_profile.cpp)
+enum ProfKind { PROF_VN = 0, PROF_CN = 1, PROF_POST = 2 };
+bool prof_armed();
+void prof_start(int kind, hipStream_t s);
+void prof_stop(hipStream_t s);
+
 // Pick the smallest compiled register-array bound that covers a degree.
 inline int deg_bucket(int d) {
     if (d <= 8) return 8;
