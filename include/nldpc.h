@@ -92,12 +92,14 @@ int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t*
  *   c2v      [B][E][Z] message state in/out: read at the start when cfg->c2v_in (otherwise a
  *            fresh all-zero state), holds the state after the last iteration on return
  *   v2c      [B][E][Z] scratch, or NULL when `saved` is given
- *   saved    [T][B][E][Z] per-iteration variable-to-check messages kept for nldpc_backward,
- *            or NULL (inference)
+ *   saved    device buffer of nldpc_saved_bytes() bytes that receives what nldpc_backward needs
+ *            (every iteration's variable-to-check messages, and for the Boosted decoders the
+ *            output clamp masks), or NULL (inference); needs every entry of `outs` non-NULL
  *   stream   hipStream_t */
+int nldpc_saved_bytes(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, size_t* bytes);
 int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
                   const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
-                  float* const* outs, const float* app_prev, float* c2v, float* v2c, float* saved,
+                  float* const* outs, const float* app_prev, float* c2v, float* v2c, void* saved,
                   void* stream);
 
 /* ---- decode backward (config 5: training through the unrolled decoder; the reference gets this
@@ -106,14 +108,14 @@ int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t
  *   grad_outs  host array of T device pointers [B][N*Z] (NULL entry = zero gradient)
  *   saved      as written by nldpc_forward
  *   g_w_cn, g_w_ucn, g_bias: [T][E] accumulated (+=) per-edge gradients, NULL if not wanted
- *   g_w_vn     [T][N] accumulated (+=) per-column gradients, NULL if not wanted
+ *   g_w_vn     [vn_prefix + T][N] accumulated (+=) per-column gradients, NULL if not wanted
  *   work       device scratch of nldpc_backward_workspace() bytes */
 int nldpc_backward_workspace(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T,
                              size_t* bytes);
 int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
                    const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
                    const float* const* outs, const float* const* grad_outs, const float* app_prev,
-                   const float* saved, float* g_w_cn, float* g_w_ucn, float* g_bias, float* g_w_vn,
+                   const void* saved, float* g_w_cn, float* g_w_ucn, float* g_bias, float* g_w_vn,
                    void* work, size_t work_bytes, void* stream);
 
 /* ---- BER/FER accounting: replaces Functions.evaluate_ber_fer (Functions.py:85-102) and the

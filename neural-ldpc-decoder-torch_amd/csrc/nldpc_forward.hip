@@ -13,8 +13,7 @@
 // Message state is [B][E][Z] fp32 in HBM with E in C-order; see DESIGN.md for the roofline.
 #include <hip/hip_runtime.h>
 
-#include "nldpc_internal.h"
-#include "nldpc_math.h"
+#include "nldpc_node.h"
 
 namespace nldpc {
 
@@ -25,8 +24,9 @@ struct VNArgs {
     const float* c2v;    // [B][E][Z] or nullptr (all-zero state)
     float* v2c;          // [B][E][Z] or nullptr (posterior only)
     float* post;         // [B][N][Z] or nullptr
-    const float* w_vn;   // [T][N] cumulative VN weights (boosted) or nullptr
-    int32_t n_vn_steps;  // number of cumulative weighting/quantisation steps for xin (k + 1)
+    uint8_t* ymask;      // [B][N][Z] clamp mask of the posterior (training) or nullptr
+    const float* w_vn;   // [steps][N] cumulative VN weights (boosted) or nullptr
+    int32_t n_vn_steps;  // number of cumulative weighting/quantisation steps for xin
     int32_t qbit;
     float lo, hi;
 };
@@ -47,42 +47,6 @@ struct CNArgs {
     int32_t qbit;
     float lo, hi;
 };
-
-// xin for the k-th iteration of a call: Q(...Q(Q(xa*w0)*w1)...) (Boosted…py:325-337).
-template <int KIND>
-__device__ __forceinline__ float vn_channel(float xa, const float* w_vn, int N, int j, int steps, int qbit) {
-    if (KIND == NLDPC_NEURAL) return xa;
-    float x = xa;
-    if (w_vn) {
-        for (int s = 0; s < steps; ++s) {
-            x = fmul(x, w_vn[(int64_t)s * N + j]);
-            if (KIND == NLDPC_QMS) x = quantize(x, qbit);
-        }
-    } else if (KIND == NLDPC_QMS) {
-        x = quantize(x, qbit);  // idempotent: Q applied every iteration equals Q applied once
-    }
-    return x;
-}
-
-// Launch geometry shared by both kernels: blockDim = (Vt copies, Bt codewords); grid =
-// (ceil(B/Bt), nodes, ceil(Z/Vt)).  The node index (column j / check row i) is blockIdx.y, so a
-// workgroup works on one node and every graph-table load is wave-uniform (scalar); lanes run
-// along consecutive lifted copies v / h, so each wave touches 64 consecutive floats of a message row.
-struct Geo {
-    int v;      // lifted copy
-    int node;   // column j (VN) or check row i (CN)
-    int64_t b;  // codeword
-    bool ok;
-};
-
-__device__ __forceinline__ Geo geo(int64_t B, int Z) {
-    Geo g;
-    g.v = blockIdx.z * blockDim.x + threadIdx.x;
-    g.node = blockIdx.y;
-    g.b = (int64_t)blockIdx.x * blockDim.y + threadIdx.y;
-    g.ok = g.v < Z && g.b < B;
-    return g;
-}
 
 template <int DV, int KIND>
 __global__ __launch_bounds__(512) void vn_kernel(VNArgs a) {
@@ -116,7 +80,9 @@ __global__ __launch_bounds__(512) void vn_kernel(VNArgs a) {
             y = fadd(xav, P);
         } else {
             const float xo = (KIND == NLDPC_QMS) ? quantize(xav, a.qbit) : xav;
-            y = clampf(fadd(xo, P), a.lo, a.hi);
+            const float yp = fadd(xo, P);
+            y = clampf(yp, a.lo, a.hi);
+            if (a.ymask) a.ymask[idx] = (uint8_t)in_range(yp, a.lo, a.hi);
         }
         a.post[idx] = y;
     }
@@ -141,7 +107,7 @@ __global__ __launch_bounds__(512) void vn_kernel(VNArgs a) {
 
 template <int DC, int KIND, bool UCN>
 __global__ __launch_bounds__(512) void cn_kernel(CNArgs a) {
-    const int Z = a.g.Z, E = a.g.E, N = a.g.N;
+    const int Z = a.g.Z, E = a.g.E;
     const Geo q = geo(a.B, Z);
     if (!q.ok) return;
     const int h = q.v, i = q.node;
@@ -155,7 +121,7 @@ __global__ __launch_bounds__(512) void cn_kernel(CNArgs a) {
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
         if (k < d) {
-            int t = h + a.g.e_shift[beg + k];
+            const int t = h + a.g.e_shift[beg + k];
             vv[k] = t >= Z ? t - Z : t;
             m[k] = a.v2c[(base + beg + k) * Z + vv[k]];
         } else {
@@ -163,138 +129,25 @@ __global__ __launch_bounds__(512) void cn_kernel(CNArgs a) {
             m[k] = 0.f;
         }
     }
-
-    // unsatisfied-check flag of (i, h): odd number of row variables with APP >= 0 (Boosted…py:346-359)
-    float u = 0.f;
-    if (UCN) {
-        int par = 0;
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            if (k < d) {
-                const int j = a.g.e_var[beg + k];
-                const int64_t off = (b * N + j) * Z + vv[k];
-                float app;
-                if (a.app) {
-                    app = a.app[off];
-                } else {
-                    app = a.xa[off];
-                    if (a.w_vn0) app = fmul(app, a.w_vn0[j]);
-                    if (KIND == NLDPC_QMS) app = quantize(app, a.qbit);
-                }
-                par ^= (-app <= 0.f) ? 1 : 0;
-            }
-        }
-        u = par ? 1.f : 0.f;
-    }
-
-    float out0[DC];
-    if (KIND == NLDPC_SP) {
-        float tv[DC];
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            if (k < d) {
-                const float x = clampf(m[k], a.lo, a.hi);
-                float t = tanhf(fmul(-0.5f, x));
-                tv[k] = fadd(t, (fabsf(t) > 0.f) ? 0.f : 1.f);
-            } else {
-                tv[k] = 1.f;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            if (k < d) {
-                float P = 1.f;
-#pragma unroll
-                for (int l = 0; l < DC; ++l)
-                    if (l < d && l != k) P = fmul(P, tv[l]);
-                P = clampf(P, -kSpClip, kSpClip);
-                out0[k] = fmul(-2.f, atanhf(P));
-            } else {
-                out0[k] = 0.f;
-            }
-        }
-    } else {
-        float min1 = kMaskMag, min2 = kMaskMag;
-        int idx1 = -1;
-        unsigned npos = 0;
-        unsigned posm = 0;
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            if (k < d) {
-                float x = m[k];
-                if (KIND == NLDPC_QMS) x = quantize(x, a.qbit);
-                if (KIND == NLDPC_MS) x = clampf(x, a.lo, a.hi);
-                if (KIND != NLDPC_NEURAL) x = fadd(x, fmul(kZeroFix, (fabsf(x) > 0.f) ? 0.f : 1.f));
-                const float ax = fabsf(x);
-                const unsigned pos = x > 0.f;
-                npos ^= pos;
-                posm |= pos << k;
-                if (ax > 0.f) {  // exact zeros are masked out of the min (Neural only; Boosted has none)
-                    if (ax < min1) {
-                        min2 = min1;
-                        min1 = ax;
-                        idx1 = k;
-                    } else if (ax < min2) {
-                        min2 = ax;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            if (k < d) {
-                float mag = (k == idx1) ? min2 : min1;
-                if (KIND != NLDPC_NEURAL) mag = (mag > kZeroFix) ? mag : fadd(mag, -kZeroFix);
-                const float sgn = ((npos ^ (posm >> k)) & 1u) ? 1.f : -1.f;
-                out0[k] = fmul(mag, sgn);
-            } else {
-                out0[k] = 0.f;
-            }
-        }
-    }
-
+    const float u = UCN ? ucn_flag<DC, KIND>(a.g, beg, d, vv, b, a.app, a.xa, a.w_vn0, a.qbit) : 0.f;
+    CnCore<DC> core;
+    cn_core<DC, KIND>(m, d, a.qbit, a.lo, a.hi, core);
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
         if (k < d) {
             const int e = beg + k;
-            const float x = out0[k];
-            const float ax = fabsf(x);
-            float r;
-            if (KIND == NLDPC_NEURAL) {
-                float t = fadd(fmul(ax, a.w_cn[e]), a.bias[e]);  // two roundings (:89)
-                r = fmul(relu_mask(t), signf_t(x));
-            } else {
-                float x1;
-                if (!a.w_cn) {
-                    x1 = ax;
-                } else if (UCN && a.w_ucn) {
-                    const float x11 = fmul(ax, a.w_cn[e]);
-                    const float x12 = fmul(ax, a.w_ucn[e]);
-                    x1 = fadd(fmul(x11, fadd(-u, 1.f)), fmul(x12, u));
-                } else {
-                    x1 = fmul(ax, a.w_cn[e]);
-                }
-                float x2 = relu_mask(x1);
-                x2 = (KIND == NLDPC_QMS) ? quantize(x2, a.qbit) : clampf(x2, a.lo, a.hi);
-                r = fmul(x2, signf_t(x));
-            }
-            a.c2v[(base + e) * Z + vv[k]] = r;
+            const CnEpi r = cn_epilogue<KIND, UCN>(core.out0[k], a.w_cn ? a.w_cn[e] : 1.f,
+                                                   a.w_ucn ? a.w_ucn[e] : 0.f, a.bias ? a.bias[e] : 0.f, u,
+                                                   a.w_cn != nullptr, a.w_ucn != nullptr, a.qbit, a.lo, a.hi);
+            a.c2v[(base + e) * Z + vv[k]] = r.c;
         }
     }
-}
-
-static void geometry(int64_t B, int Z, int nodes, dim3& grid, dim3& block) {
-    const int vt = Z <= 512 ? Z : 256;
-    int bt = 256 / vt;
-    if (bt < 1) bt = 1;
-    block = dim3(vt, bt, 1);
-    grid = dim3((unsigned)((B + bt - 1) / bt), (unsigned)nodes, (unsigned)((Z + vt - 1) / vt));
 }
 
 template <int DV, int KIND>
 static hipError_t launch_vn(const VNArgs& a, hipStream_t s) {
     dim3 grid, block;
-    geometry(a.B, a.g.Z, a.g.N, grid, block);
+    node_geometry(a.B, a.g.Z, a.g.N, grid, block);
     hipLaunchKernelGGL((vn_kernel<DV, KIND>), grid, block, 0, s, a);
     return hipGetLastError();
 }
@@ -302,7 +155,7 @@ static hipError_t launch_vn(const VNArgs& a, hipStream_t s) {
 template <int DC, int KIND, bool UCN>
 static hipError_t launch_cn(const CNArgs& a, hipStream_t s) {
     dim3 grid, block;
-    geometry(a.B, a.g.Z, a.g.M, grid, block);
+    node_geometry(a.B, a.g.Z, a.g.M, grid, block);
     hipLaunchKernelGGL((cn_kernel<DC, KIND, UCN>), grid, block, 0, s, a);
     return hipGetLastError();
 }
@@ -317,7 +170,7 @@ static hipError_t dispatch_vn(int dv, const VNArgs& a, hipStream_t s) {
     }
 }
 
-hipError_t vn_launch(int kind, const VNArgs& a, hipStream_t s) {
+static hipError_t vn_launch(int kind, const VNArgs& a, hipStream_t s) {
     switch (kind) {
         case NLDPC_NEURAL: return dispatch_vn<NLDPC_NEURAL>(a.g.max_dv, a, s);
         case NLDPC_SP: return dispatch_vn<NLDPC_SP>(a.g.max_dv, a, s);
@@ -341,7 +194,7 @@ static hipError_t dispatch_cn(bool ucn, const CNArgs& a, hipStream_t s) {
     return ucn ? dispatch_cn2<KIND, true>(a, s) : dispatch_cn2<KIND, false>(a, s);
 }
 
-hipError_t cn_launch(int kind, bool ucn, const CNArgs& a, hipStream_t s) {
+static hipError_t cn_launch(int kind, bool ucn, const CNArgs& a, hipStream_t s) {
     switch (kind) {
         case NLDPC_NEURAL: return dispatch_cn2<NLDPC_NEURAL, false>(a, s);
         case NLDPC_SP: return dispatch_cn<NLDPC_SP>(ucn, a, s);
@@ -358,16 +211,39 @@ int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t 
     if (cfg->kind == NLDPC_NEURAL && (cfg->ucn || cfg->vn_cumulative))
         return fail(NLDPC_EINVAL, "the Neural decoder has no UCN / VN weighting");
     if (B > 0x7FFFFFFFLL) return fail(NLDPC_EUNSUPPORTED, "batch too large for one launch (split the batch)");
+    if (cfg->vn_prefix < 0 || (cfg->vn_prefix > 0 && !cfg->vn_cumulative))
+        return fail(NLDPC_EINVAL, "vn_prefix needs vn_cumulative");
     return NLDPC_OK;
+}
+
+SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T) {
+    SavedLayout L;
+    const int64_t EZ = (int64_t)g->dev.E * g->dev.Z, NZ = (int64_t)g->dev.N * g->dev.Z;
+    L.v2c_off = 0;
+    L.v2c_stride = B * EZ;  // floats per iteration
+    const size_t v2c_bytes = (size_t)T * B * EZ * sizeof(float);
+    L.ymask_off = (v2c_bytes + 255) & ~(size_t)255;
+    L.ymask_stride = B * NZ;  // bytes per iteration
+    L.has_ymask = cfg->kind != NLDPC_NEURAL;
+    L.total = L.has_ymask ? L.ymask_off + (size_t)T * B * NZ : v2c_bytes;
+    return L;
 }
 
 }  // namespace nldpc
 
 using namespace nldpc;
 
+extern "C" int nldpc_saved_bytes(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, size_t* bytes) {
+    int st = validate_cfg(g, cfg, B, T);
+    if (st) return st;
+    if (!bytes) return fail(NLDPC_EINVAL, "nldpc_saved_bytes: null output");
+    *bytes = saved_layout(g, cfg, B, T).total;
+    return NLDPC_OK;
+}
+
 extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
                              const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
-                             float* const* outs, const float* app_prev, float* c2v, float* v2c, float* saved,
+                             float* const* outs, const float* app_prev, float* c2v, float* v2c, void* saved,
                              void* stream) {
     int st = validate_cfg(g, cfg, B, T);
     if (st) return st;
@@ -382,21 +258,26 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
             return fail(NLDPC_EINVAL, "nldpc_forward: UCN after iteration 0 needs app_prev");
     }
     if (cfg->vn_cumulative && !w_vn) return fail(NLDPC_EINVAL, "nldpc_forward: vn_cumulative needs w_vn");
-    if (cfg->vn_prefix < 0 || (cfg->vn_prefix > 0 && !cfg->vn_cumulative))
-        return fail(NLDPC_EINVAL, "nldpc_forward: vn_prefix needs vn_cumulative");
+    if (saved) {
+        for (int k = 0; k < T; ++k)
+            if (!outs[k]) return fail(NLDPC_EINVAL, "nldpc_forward: saving for backward needs every output");
+    }
     DeviceGuard guard(g->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const DevGraph& G = g->dev;
-    const int64_t EZ = (int64_t)G.E * G.Z;
+    const SavedLayout SL = saved_layout(g, cfg, B, T);
+    float* saved_v2c = saved ? reinterpret_cast<float*>(static_cast<char*>(saved) + SL.v2c_off) : nullptr;
+    uint8_t* saved_mask = (saved && SL.has_ymask) ? static_cast<uint8_t*>(saved) + SL.ymask_off : nullptr;
     bool state_valid = cfg->c2v_in != 0;
     for (int k = 0; k < T; ++k) {
-        float* v2c_k = saved ? saved + (int64_t)k * B * EZ : v2c;
+        float* v2c_k = saved_v2c ? saved_v2c + (int64_t)k * SL.v2c_stride : v2c;
         VNArgs va{G,
                   B,
                   xa,
                   state_valid ? c2v : nullptr,
                   v2c_k,
                   k >= 1 ? outs[k - 1] : nullptr,
+                  (k >= 1 && saved_mask) ? saved_mask + (int64_t)(k - 1) * SL.ymask_stride : nullptr,
                   cfg->vn_cumulative ? w_vn : nullptr,
                   cfg->vn_prefix + k + 1,
                   cfg->qbit,
@@ -428,7 +309,9 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
         state_valid = true;
     }
     if (outs[T - 1]) {
-        VNArgs va{G, B, xa, c2v, nullptr, outs[T - 1], nullptr, 0, cfg->qbit, cfg->llr_lo, cfg->llr_hi};
+        VNArgs va{G, B, xa, c2v, nullptr, outs[T - 1],
+                  saved_mask ? saved_mask + (int64_t)(T - 1) * SL.ymask_stride : nullptr, nullptr, 0, cfg->qbit,
+                  cfg->llr_lo, cfg->llr_hi};
         prof_start(PROF_POST, s);
         hipError_t e = vn_launch(cfg->kind, va, s);
         prof_stop(s);

@@ -56,6 +56,17 @@ struct DeviceGuard {
     }
 };
 
+// Layout of the `saved` buffer nldpc_forward fills for nldpc_backward:
+//   v2c   [T][B][E][Z] fp32 variable-to-check messages of every iteration
+//   ymask [T][B][N][Z] uint8 clamp mask of every posterior (Boosted decoders only)
+struct SavedLayout {
+    size_t v2c_off, ymask_off, total;
+    int64_t v2c_stride, ymask_stride;
+    bool has_ymask;
+};
+SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T);
+int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T);
+
 // benchmark instrumentation (nldpc_profile.cpp)
 enum ProfKind { PROF_VN = 0, PROF_CN = 1, PROF_POST = 2 };
 bool prof_armed();

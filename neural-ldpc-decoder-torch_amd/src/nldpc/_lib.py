@@ -25,7 +25,7 @@ ABI_VERSION = 1
 # every symbol include/nldpc.h declares
 EXPORTED = (
     "nldpc_abi_version", "nldpc_last_error", "nldpc_graph_create", "nldpc_graph_destroy", "nldpc_graph_dims",
-    "nldpc_graph_edges", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
+    "nldpc_graph_edges", "nldpc_saved_bytes", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
     "nldpc_awgn_llr", "nldpc_profile_begin", "nldpc_profile_end",
 )
 
@@ -70,6 +70,7 @@ def _declare(lib):
         "nldpc_graph_destroy": (_i32, [_vp]),
         "nldpc_graph_dims": (_i32, [_vp, ctypes.POINTER(_i32)]),
         "nldpc_graph_edges": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+        "nldpc_saved_bytes": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, ctypes.POINTER(ctypes.c_size_t)]),
         "nldpc_forward": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _vp, _vp, _vp, _vp, _vp, _PP, _vp, _vp,
                                  _vp, _vp, _vp]),
         "nldpc_backward_workspace": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, ctypes.POINTER(ctypes.c_size_t)]),

@@ -50,7 +50,7 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
            w_vn=None, c2v=None, app_prev=None, save=False, out_mask=None):
     """Run T iterations.  xa [B, N, Z] fp32 device tensor.  Weights: [T, E] / [T, N] tensors or None.
 
-    Returns (outputs [T, B, N*Z], c2v state [B, E, Z], saved [T, B, E, Z] or None).
+    Returns (outputs [T, B, N*Z], c2v state [B, E, Z], saved byte buffer for the backward or None).
     c2v: optional incoming state [B, E, Z] (None = all-zero messages)."""
     _require_device_tensor(xa, "xa")
     if xa.dim() != 3 or xa.shape[1] != graph.N or xa.shape[2] != graph.Z:
@@ -66,15 +66,20 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
     else:
         state = c2v.detach().to(torch.float32).contiguous().clone()
         c2v_in = True
-    saved = torch.empty((T, B, E, Z), dtype=torch.float32, device=dev) if save else None
+    c = cfg.c_struct(c2v_in)
+    L = _lib.lib()
+    h = graph.handle(dev)
+    saved = None
+    if save:
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(L.nldpc_saved_bytes(h, ctypes.byref(c), B, T, ctypes.byref(nbytes)), "nldpc_saved_bytes")
+        saved = torch.empty((int(nbytes.value),), dtype=torch.uint8, device=dev)
     scratch = None if save else torch.empty((B, E, Z), dtype=torch.float32, device=dev)
     tensors = [None if (out_mask is not None and not out_mask[t]) else outs[t] for t in range(T)]
     pp, keep = _lib.ptr_array(tensors)
     w_cn, w_ucn, bias, w_vn = _f32c(w_cn), _f32c(w_ucn), _f32c(bias), _f32c(w_vn)
     app = _f32c(app_prev)
-    c = cfg.c_struct(c2v_in)
-    L = _lib.lib()
-    st = L.nldpc_forward(graph.handle(dev), ctypes.byref(c), B, T, _lib.ptr(xa_c), _lib.ptr(w_cn), _lib.ptr(w_ucn),
+    st = L.nldpc_forward(h, ctypes.byref(c), B, T, _lib.ptr(xa_c), _lib.ptr(w_cn), _lib.ptr(w_ucn),
                          _lib.ptr(bias), _lib.ptr(w_vn), pp, _lib.ptr(app), _lib.ptr(state), _lib.ptr(scratch),
                          _lib.ptr(saved), _lib.stream_of(dev))
     del keep
@@ -87,12 +92,13 @@ def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, 
     """Gradients of the per-edge / per-column weights.  Returns (g_w_cn, g_w_ucn, g_bias, g_w_vn)."""
     dev = xa.device
     B = int(xa.shape[0])
-    E, N = graph.E, graph.N
-    z = lambda shape, on: torch.zeros(shape, dtype=torch.float32, device=dev) if on else None  # noqa: E731
-    g_cn = z((T, E), w_cn is not None and need[0])
-    g_ucn = z((T, E), w_ucn is not None and need[1])
-    g_b = z((T, E), bias is not None and need[2])
-    g_vn = z((T, N), w_vn is not None and need[3])
+    def z(ref, on):
+        return torch.zeros(tuple(ref.shape), dtype=torch.float32, device=dev) if (ref is not None and on) else None
+
+    g_cn = z(w_cn, need[0])
+    g_ucn = z(w_ucn, need[1])
+    g_b = z(bias, need[2])
+    g_vn = z(w_vn, need[3])
     c = cfg.c_struct(False)
     L = _lib.lib()
     h = graph.handle(dev)
