@@ -57,14 +57,8 @@ def kernel_bytes(B, E, N, Z, T):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from nldpc import distributed as nd_dist
+    rank, world, local = nd_dist.init("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -80,12 +74,13 @@ def main():
     E = int(conn.sum_edge)
     rate = (N - M) / (N - 2)  # reference code-rate formula (AWGNPassedDatagen.py:47 / neural :36) = 0.2
     sigma = sigma_for(args.ebn0, rate)
-    xa = awgn_llr(B, N, Z, sigma, seed=2042, b_offset=rank * B, device=dev)
+    # weak scaling: every rank decodes B codewords; rank r holds global codewords [r*B, (r+1)*B)
+    offset, _ = nd_dist.shard(world * B, rank, world)
+    xa = awgn_llr(B, N, Z, sigma, seed=2042, b_offset=offset, device=dev)
     torch.cuda.synchronize(dev)
 
     def barrier():
-        if dist:
-            tdist.barrier(device_ids=[local])
+        nd_dist.barrier(local)
 
     outs = None
     with torch.no_grad():
@@ -117,12 +112,8 @@ def main():
 
         # BER / FER of every iteration on this rank's codewords (decoder convention bit = LLR > 0)
         counts = ber_counts(outs)
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist:
-        tdist.all_reduce(t_max, op=tdist.ReduceOp.MAX)
-        tdist.all_reduce(counts, op=tdist.ReduceOp.SUM)  # the one RCCL exchange: BER accounting
-    elapsed = float(t_max.item())
-    counts = counts.cpu().numpy()
+    elapsed = nd_dist.max_time(elapsed, device=dev)
+    counts = nd_dist.sum_counts(counts).cpu().numpy()  # the one RCCL exchange: BER accounting
 
     result = None
     if rank == 0:
@@ -182,9 +173,8 @@ def main():
             res["cpu_baseline"] = cpu_baseline(bg, Z, T, sigma, args.cpu_seconds)
         result = res
         print(json.dumps(result), flush=True)
-    if dist:
-        tdist.barrier(device_ids=[local])
-        tdist.destroy_process_group()
+    barrier()
+    nd_dist.finalize()
     return result
 
 
