@@ -46,13 +46,21 @@ def parse():
 
 
 def kernel_bytes(B, E, N, Z, T):
-    """Algorithmic HBM bytes per launch kind: fp32 messages streamed once."""
+    """Algorithmic HBM bytes of one decode (all launches of a kind together), DESIGN.md §Roofline.
+
+    fused: SURVEY.md §8(d) D5's per-codeword figure 4*(2*T*E*Z + (T+1)*N*Z) (a flooding decoder whose
+    message state is streamed once per iteration, plus the channel and the T posteriors) x B — the
+    figure the metric's roofline is defined on; the register-resident kernel moves only the
+    compulsory part 4*(T+1)*N*Z itself (reported separately, and measured by PMC in profiles/).
+    vn/cn/post: the streaming kernels' own fp32 message traffic."""
     f = 4
     vn_first = B * f * (E * Z + N * Z)            # read xa, write v2c (all-zero state: no c2v read)
     vn = B * f * (2 * E * Z + 2 * N * Z)          # read c2v + xa, write v2c + previous posterior
     cn = B * f * (2 * E * Z)                      # gather v2c, scatter c2v
     post = B * f * (E * Z + 2 * N * Z)            # read c2v + xa, write the last posterior
-    return {"vn": vn_first + (T - 1) * vn, "cn": T * cn, "post": post}
+    fused = B * f * (2 * T * E * Z + (T + 1) * N * Z)
+    return {"vn": vn_first + (T - 1) * vn, "cn": T * cn, "post": post, "fused": fused,
+            "fused_compulsory": B * f * (T + 1) * N * Z}
 
 
 def main():
@@ -91,7 +99,7 @@ def main():
         barrier()
         torch.cuda.synchronize(dev)
         L = _lib.lib()
-        launches = args.steps * (2 * T + 1)
+        launches = args.steps * (2 * T + 2)
         if not args.no_profile:
             _lib.check(L.nldpc_profile_begin(launches), "nldpc_profile_begin")
         t0 = time.perf_counter()
@@ -105,10 +113,10 @@ def main():
         prof = None
         if not args.no_profile:
             import ctypes
-            ms = (ctypes.c_float * 3)()
-            cnt = (ctypes.c_int32 * 3)()
-            _lib.check(L.nldpc_profile_end(3, ms, cnt), "nldpc_profile_end")
-            prof = {"vn": (ms[0], cnt[0]), "cn": (ms[1], cnt[1]), "post": (ms[2], cnt[2])}
+            ms = (ctypes.c_float * 4)()
+            cnt = (ctypes.c_int32 * 4)()
+            _lib.check(L.nldpc_profile_end(4, ms, cnt), "nldpc_profile_end")
+            prof = {"vn": (ms[0], cnt[0]), "cn": (ms[1], cnt[1]), "post": (ms[2], cnt[2]), "fused": (ms[3], cnt[3])}
 
         # BER / FER of every iteration on this rank's codewords (decoder convention bit = LLR > 0)
         counts = ber_counts(outs)
@@ -144,13 +152,15 @@ def main():
         if prof is not None:
             kb = kernel_bytes(B, E, N, Z, T)
             per = {}
-            for k in ("vn", "cn", "post"):
+            for k in ("vn", "cn", "post", "fused"):
                 ms_tot, n = prof[k]
                 if n:
                     byts = kb[k] * args.steps
                     per[k] = {"avg_ms": ms_tot / n, "launches": n, "gbs": byts / (ms_tot / 1000.0) / 1e9,
                               "alg_bytes_per_launch": byts / n}
-            dom = max(("vn", "cn"), key=lambda k: prof[k][0])
+                    if k == "fused":
+                        per[k]["compulsory_gbs"] = kb["fused_compulsory"] * args.steps / (ms_tot / 1000.0) / 1e9
+            dom = max(per, key=lambda k: prof[k][0])
             d = per[dom]
             traffic = None
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -161,7 +171,8 @@ def main():
                     traffic = pj.get(key)
                 except Exception:
                     traffic = None
-            res["roofline"] = {"bound": "hbm", "kernel": {"vn": "vn_kernel", "cn": "cn_kernel"}[dom],
+            res["roofline"] = {"bound": "hbm", "kernel": {"vn": "vn_kernel", "cn": "cn_kernel", "post": "vn_kernel",
+                                                          "fused": "fused_bg2_z384::kernel"}[dom],
                                "achieved": round(d["gbs"], 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": round(d["gbs"] / PEAK_HBM_GBS, 4), "traffic": traffic,
                                "alg_bytes_per_launch": d["alg_bytes_per_launch"], "avg_launch_ms": round(d["avg_ms"], 4),

@@ -57,8 +57,14 @@ typedef struct nldpc_cfg {
     int32_t c2v_in;  /* 1: read the c2v state at the start; 0: start from all-zero messages */
     int32_t vn_prefix; /* rows of w_vn applied before this call's first iteration (cumulative VN
                           weighting carried over earlier iterations of the same forward) */
-    int32_t reserved;
+    int32_t flags;   /* NLDPC_FLAG_* */
 } nldpc_cfg;
+
+/* cfg->flags */
+#define NLDPC_FLAG_STREAM 1      /* force the streaming (two kernels per iteration) path */
+#define NLDPC_FLAG_FUSED 2       /* require the register-resident fused path (error if ineligible) */
+#define NLDPC_FLAG_NO_STATE 4    /* the caller does not need the final c2v state: c2v may be NULL
+                                    when the fused path runs */
 
 /* ---- library ---------------------------------------------------------------------------- */
 int nldpc_abi_version(void);
@@ -75,6 +81,13 @@ int nldpc_graph_destroy(nldpc_graph* g);
 int nldpc_graph_dims(const nldpc_graph* g, int32_t* dims);
 /* host copies of the C-order edge tables: check, variable, shift (mod Z) of every edge */
 int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t* shift);
+
+/* ---- execution path.  *eligible = 1 when nldpc_forward with these arguments runs the fused
+ *      register-resident kernel (a base graph / lifting size compiled in, no UCN, fresh state,
+ *      T <= 64, not saving for backward): then v2c is unused, and c2v is unused too with
+ *      NLDPC_FLAG_NO_STATE.  Otherwise the streaming kernels run and need both buffers. */
+int nldpc_fast_path(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, int32_t saving,
+                    int32_t* eligible);
 
 /* ---- decode forward: replaces NeuralLDPCDecoder.forward (NeuralLDPCDecoder.py:44-100) and
  *      BoostedNeuralLDPCDecoder.forward (BoostedNeuralLDPCDecoder.py:260-538).

@@ -13,7 +13,9 @@
 // Message state is [B][E][Z] fp32 in HBM with E in C-order; see DESIGN.md for the roofline.
 #include <hip/hip_runtime.h>
 
-#include "nldpc_node.h"
+#include <cstdlib>
+
+#include "nldpc_fused.h"
 
 namespace nldpc {
 
@@ -229,9 +231,51 @@ SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     return L;
 }
 
+static bool fused_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T, bool saving) {
+    static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
+    if (disabled || (cfg->flags & NLDPC_FLAG_STREAM)) return false;
+    return g->fused >= 0 && !saving && !cfg->ucn && !cfg->c2v_in && T <= kFusedMaxT;
+}
+
+static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
+                         const float* w_cn, const float* bias, const float* w_vn, float* const* outs, float* c2v,
+                         hipStream_t s) {
+    int n = 0;
+    const FusedSpec& f = fused_specs(&n)[g->fused];
+    FusedArgs fa{};
+    fa.B = B;
+    fa.T = T;
+    fa.qbit = cfg->qbit;
+    fa.xa = xa;
+    fa.w_cn = w_cn;
+    fa.bias = bias;
+    fa.w_vn = cfg->vn_cumulative ? w_vn : nullptr;
+    fa.vn_prefix = cfg->vn_prefix;
+    fa.lo = cfg->llr_lo;
+    fa.hi = cfg->llr_hi;
+    fa.c2v_out = (cfg->flags & NLDPC_FLAG_NO_STATE) ? nullptr : c2v;
+    for (int k = 0; k < kFusedMaxT; ++k) fa.outs.p[k] = k < T ? outs[k] : nullptr;
+    void* args[] = {&fa};
+    const int64_t blocks = (B + f.G - 1) / f.G;
+    prof_start(PROF_FUSED, s);
+    hipError_t e = hipLaunchKernel(f.kernels[cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args, 0, s);
+    prof_stop(s);
+    if (e == hipSuccess) e = hipGetLastError();
+    return e == hipSuccess ? NLDPC_OK : hip_fail(e, "fused kernel launch");
+}
+
 }  // namespace nldpc
 
 using namespace nldpc;
+
+extern "C" int nldpc_fast_path(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, int32_t saving,
+                               int32_t* eligible) {
+    int st = validate_cfg(g, cfg, B, T);
+    if (st) return st;
+    if (!eligible) return fail(NLDPC_EINVAL, "nldpc_fast_path: null output");
+    *eligible = fused_eligible(g, cfg, T, saving != 0) ? 1 : 0;
+    return NLDPC_OK;
+}
 
 extern "C" int nldpc_saved_bytes(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, size_t* bytes) {
     int st = validate_cfg(g, cfg, B, T);
@@ -247,8 +291,7 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
                              void* stream) {
     int st = validate_cfg(g, cfg, B, T);
     if (st) return st;
-    if (!xa || !c2v || !outs) return fail(NLDPC_EINVAL, "nldpc_forward: xa, c2v and outs are required");
-    if (!v2c && !saved) return fail(NLDPC_EINVAL, "nldpc_forward: need v2c scratch or saved buffer");
+    if (!xa || !outs) return fail(NLDPC_EINVAL, "nldpc_forward: xa and outs are required");
     if (cfg->kind == NLDPC_NEURAL && (!w_cn || !bias))
         return fail(NLDPC_EINVAL, "nldpc_forward: the Neural decoder needs w_cn and bias");
     if (cfg->ucn) {
@@ -264,6 +307,16 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
     }
     DeviceGuard guard(g->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool fused = fused_eligible(g, cfg, T, saved != nullptr);
+    if ((cfg->flags & NLDPC_FLAG_FUSED) && !fused)
+        return fail(NLDPC_EUNSUPPORTED, "nldpc_forward: the fused path is not available for this call");
+    if (fused) {
+        if (!c2v && !(cfg->flags & NLDPC_FLAG_NO_STATE))
+            return fail(NLDPC_EINVAL, "nldpc_forward: c2v is required unless NLDPC_FLAG_NO_STATE");
+        return fused_forward(g, cfg, B, T, xa, w_cn, bias, w_vn, outs, c2v, s);
+    }
+    if (!c2v) return fail(NLDPC_EINVAL, "nldpc_forward: c2v is required by the streaming path");
+    if (!v2c && !saved) return fail(NLDPC_EINVAL, "nldpc_forward: need v2c scratch or saved buffer");
     const DevGraph& G = g->dev;
     const SavedLayout SL = saved_layout(g, cfg, B, T);
     float* saved_v2c = saved ? reinterpret_cast<float*>(static_cast<char*>(saved) + SL.v2c_off) : nullptr;

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "nldpc_fused.h"
 #include "nldpc_internal.h"
 
 namespace nldpc {
@@ -104,6 +105,21 @@ extern "C" int nldpc_graph_create(int32_t M, int32_t N, int32_t Z, const int32_t
         }
         nldpc_graph* g = new nldpc_graph();
         g->device = device;
+        g->fused = -1;
+        {  // a generated fused kernel for exactly this lifted graph? (same M, N, Z and edge shifts)
+            int nspec = 0;
+            const FusedSpec* specs = fused_specs(&nspec);
+            for (int k = 0; k < nspec && g->fused < 0; ++k) {
+                const FusedSpec& f = specs[k];
+                if (f.M != M || f.N != N || f.Z != Z) continue;
+                bool same = true;
+                for (int64_t q = 0; q < (int64_t)M * N && same; ++q) {
+                    const int32_t a = basegraph[q], b = f.basegraph[q];
+                    same = (a == -1) == (b == -1) && (a == -1 || (a % Z) == (b % Z));
+                }
+                if (same) g->fused = k;
+            }
+        }
         g->blob = d_blob;
         const int32_t* base = static_cast<const int32_t*>(d_blob);
         g->dev = DevGraph{M, N, Z, E, max_dc, max_dv, base + off_chk, base + off_var, base + off_shift,

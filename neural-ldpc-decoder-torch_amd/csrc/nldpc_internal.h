@@ -29,6 +29,7 @@ struct DevGraph {
 struct nldpc_graph {
     nldpc::DevGraph dev;
     int32_t device;
+    int32_t fused;  // index into nldpc::fused_specs() of a compiled register-resident kernel, or -1
     void* blob;  // device allocation backing the tables
     // host mirrors
     int32_t* h_chk;
@@ -68,7 +69,7 @@ SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
 int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T);
 
 // benchmark instrumentation (nldpc_profile.cpp)
-enum ProfKind { PROF_VN = 0, PROF_CN = 1, PROF_POST = 2 };
+enum ProfKind { PROF_VN = 0, PROF_CN = 1, PROF_POST = 2, PROF_FUSED = 3 };
 bool prof_armed();
 void prof_start(int kind, hipStream_t s);
 void prof_stop(hipStream_t s);

@@ -34,7 +34,7 @@ class NeuralLDPCDecoder(nn.Module):
             [nn.Parameter(torch.full((E,), 0.5, dtype=torch.float32)) for _ in range(iter_node_counts)])
         self.biases_var = nn.ParameterList(
             [nn.Parameter(torch.zeros(E, dtype=torch.float32)) for _ in range(iter_node_counts)])
-        self._cfg = DecodeCfg(kind=KIND_NEURAL)
+        self._cfg = DecodeCfg(kind=KIND_NEURAL, keep_state=False)  # forward() never resumes from a state
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
                               error_msgs):

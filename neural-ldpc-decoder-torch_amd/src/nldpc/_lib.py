@@ -21,11 +21,12 @@ LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libnldpc.so"
 NLDPC_OK, NLDPC_EINVAL, NLDPC_EHIP, NLDPC_EUNSUPPORTED = 0, 1, 2, 3
 NLDPC_SP, NLDPC_MS, NLDPC_QMS, NLDPC_NEURAL = 0, 1, 2, 3
 ABI_VERSION = 1
+FLAG_STREAM, FLAG_FUSED, FLAG_NO_STATE = 1, 2, 4
 
 # every symbol include/nldpc.h declares
 EXPORTED = (
     "nldpc_abi_version", "nldpc_last_error", "nldpc_graph_create", "nldpc_graph_destroy", "nldpc_graph_dims",
-    "nldpc_graph_edges", "nldpc_saved_bytes", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
+    "nldpc_graph_edges", "nldpc_fast_path", "nldpc_saved_bytes", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
     "nldpc_awgn_llr", "nldpc_profile_begin", "nldpc_profile_end",
 )
 
@@ -41,7 +42,7 @@ class NldpcCfg(ctypes.Structure):
         ("first_iter", ctypes.c_int32),
         ("c2v_in", ctypes.c_int32),
         ("vn_prefix", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
     ]
 
 
@@ -70,6 +71,7 @@ def _declare(lib):
         "nldpc_graph_destroy": (_i32, [_vp]),
         "nldpc_graph_dims": (_i32, [_vp, ctypes.POINTER(_i32)]),
         "nldpc_graph_edges": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+        "nldpc_fast_path": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _i32, ctypes.POINTER(_i32)]),
         "nldpc_saved_bytes": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, ctypes.POINTER(ctypes.c_size_t)]),
         "nldpc_forward": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _vp, _vp, _vp, _vp, _vp, _PP, _vp, _vp,
                                  _vp, _vp, _vp]),

@@ -28,11 +28,17 @@ class DecodeCfg:
     llr_hi: float = 20.0
     first_iter: int = 0
     vn_prefix: int = 0
+    path: str = "auto"        # "auto" | "stream" | "fused" (register-resident kernel)
+    keep_state: bool = True   # False: the final c2v state is not needed (lets the fused path skip it)
+
+    def flags(self) -> int:
+        f = {"auto": 0, "stream": _lib.FLAG_STREAM, "fused": _lib.FLAG_FUSED}[self.path]
+        return f | (0 if self.keep_state else _lib.FLAG_NO_STATE)
 
     def c_struct(self, c2v_in: bool) -> _lib.NldpcCfg:
         return _lib.NldpcCfg(self.kind, int(self.qbit), int(bool(self.ucn)), int(bool(self.vn_cumulative)),
                              float(self.llr_lo), float(self.llr_hi), int(self.first_iter), int(bool(c2v_in)),
-                             int(self.vn_prefix), 0)
+                             int(self.vn_prefix), self.flags())
 
 
 def _require_device_tensor(x: torch.Tensor, name: str):
@@ -60,21 +66,24 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
     xa_c = _f32c(xa)
     E, N, Z = graph.E, graph.N, graph.Z
     outs = torch.empty((T, B, N * Z), dtype=torch.float32, device=dev)
-    if c2v is None:
-        state = torch.empty((B, E, Z), dtype=torch.float32, device=dev)
-        c2v_in = False
-    else:
-        state = c2v.detach().to(torch.float32).contiguous().clone()
-        c2v_in = True
+    c2v_in = c2v is not None
     c = cfg.c_struct(c2v_in)
     L = _lib.lib()
     h = graph.handle(dev)
+    fast = ctypes.c_int32(0)
+    _lib.check(L.nldpc_fast_path(h, ctypes.byref(c), B, T, int(bool(save)), ctypes.byref(fast)), "nldpc_fast_path")
+    if c2v_in:
+        state = c2v.detach().to(torch.float32).contiguous().clone()
+    elif fast.value and not cfg.keep_state:
+        state = None
+    else:
+        state = torch.empty((B, E, Z), dtype=torch.float32, device=dev)
     saved = None
     if save:
         nbytes = ctypes.c_size_t(0)
         _lib.check(L.nldpc_saved_bytes(h, ctypes.byref(c), B, T, ctypes.byref(nbytes)), "nldpc_saved_bytes")
         saved = torch.empty((int(nbytes.value),), dtype=torch.uint8, device=dev)
-    scratch = None if save else torch.empty((B, E, Z), dtype=torch.float32, device=dev)
+    scratch = None if (save or fast.value) else torch.empty((B, E, Z), dtype=torch.float32, device=dev)
     tensors = [None if (out_mask is not None and not out_mask[t]) else outs[t] for t in range(T)]
     pp, keep = _lib.ptr_array(tensors)
     w_cn, w_ucn, bias, w_vn = _f32c(w_cn), _f32c(w_ucn), _f32c(bias), _f32c(w_vn)
@@ -136,6 +145,8 @@ class DecodeFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         if need_grad:
             ctx.save_for_backward(xa, w_cn, w_ucn, bias, w_vn, app_prev, outs, saved)
+        if state is None:
+            state = outs.new_empty((0,))
         ctx.mark_non_differentiable(state)
         return (*outs.unbind(0), state)
 

@@ -64,13 +64,14 @@ def boosted_params(d, g, T, nw, fixed):
 @pytest.mark.parametrize("name", ["neural_cfg1_snr1_default", "neural_cfg1_snr2_default", "neural_cfg1_snr3_default",
                                   "neural_cfg1_snr4_default", "neural_cfg1_snr2_random",
                                   "neural_bg2_z16_b16_t5_random", "neural_wimax_z24_b16_t20_random"])
-def test_neural_forward_matches_reference(golden, name):
+@pytest.mark.parametrize("path", ["stream", "fused"])
+def test_neural_forward_matches_reference(golden, name, path):
     from nldpc.decode import KIND_NEURAL, DecodeCfg, decode
     d = golden(name)
     g = _graph(_bg(name), int(d["Z"]))
     T = int(d["T"])
     x = torch.from_numpy(d["x"]).to(DEV)
-    outs, _, _ = decode(g, DecodeCfg(KIND_NEURAL), x, T, w_cn=torch.from_numpy(d["weights"]).to(DEV),
+    outs, _, _ = decode(g, DecodeCfg(KIND_NEURAL, path=path), x, T, w_cn=torch.from_numpy(d["weights"]).to(DEV),
                         bias=torch.from_numpy(d["biases"]).to(DEV))
     o = outs.cpu().numpy()
     assert np.array_equal(o, d["outputs"]), f"{(o != d['outputs']).sum()} of {o.size} soft values differ"
@@ -79,8 +80,9 @@ def test_neural_forward_matches_reference(golden, name):
 BOOSTED = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "boosted_*.npz")))
 
 
+@pytest.mark.parametrize("path", ["stream", "auto"])
 @pytest.mark.parametrize("name", BOOSTED)
-def test_boosted_forward_matches_reference(golden, name):
+def test_boosted_forward_matches_reference(golden, name, path):
     from nldpc.decode import DecodeCfg, decode
     d = golden(name)
     g = _graph(_bg(name), int(d["Z"]))
@@ -89,7 +91,7 @@ def test_boosted_forward_matches_reference(golden, name):
     fixed = [int(v) for v in d.get("fixed_nodes", [])]
     w_cn, w_ucn, w_vn, use_ucn = boosted_params(d, g, T, nw, fixed)
     kind, q = int(d["dtype"]), int(d["q"])
-    cfg = DecodeCfg(kind=kind, qbit=q, ucn=use_ucn, vn_cumulative=w_vn is not None)
+    cfg = DecodeCfg(kind=kind, qbit=q, ucn=use_ucn, vn_cumulative=w_vn is not None, path=path)
     x = torch.from_numpy(d["x"]).to(DEV)
     outs, _, _ = decode(g, cfg, x, T, w_cn=w_cn, w_ucn=w_ucn, w_vn=w_vn)
     o = outs.cpu().numpy()
@@ -101,8 +103,9 @@ def test_boosted_forward_matches_reference(golden, name):
         assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} soft values differ"
 
 
+@pytest.mark.parametrize("path", ["stream", "fused"])
 @pytest.mark.parametrize("B", [1, 3, 8])
-def test_neural_z384_matches_oracle(B):
+def test_neural_z384_matches_oracle(B, path):
     """BG2 z=384 (the headline graph; the reference cannot run it): GPU == CPU oracle bit for bit."""
     from nldpc.decode import KIND_NEURAL, DecodeCfg, decode
     from oracle.ldpc_oracle import OracleGraph, neural_forward
@@ -113,7 +116,40 @@ def test_neural_z384_matches_oracle(B):
     x = (2 * (-1 + sigma * torch.randn(B, 52, 384, generator=gen)) / sigma ** 2).float()
     w = torch.rand(T, g.E, generator=gen) * 1.2
     b = torch.randn(T, g.E, generator=gen) * 0.1
-    outs, _, _ = decode(g, DecodeCfg(KIND_NEURAL), x.to(DEV), T, w_cn=w.to(DEV), bias=b.to(DEV))
+    outs, _, _ = decode(g, DecodeCfg(KIND_NEURAL, path=path), x.to(DEV), T, w_cn=w.to(DEV), bias=b.to(DEV))
     ref = torch.stack(neural_forward(OracleGraph(BG2, 384), x, list(w), list(b))).numpy()
     o = outs.cpu().numpy()
     assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} differ"
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_boosted_z384_fused_equals_stream(kind):
+    """Fused (register-resident) and streaming kernels agree bit for bit at BG2 z=384, Boosted kinds,
+    with per-check CN weights, cumulative VN weights and the final message state."""
+    from nldpc.decode import DecodeCfg, decode
+    T, B = 6, 3
+    g = _graph(BG2, 384)
+    gen = torch.Generator().manual_seed(kind)
+    x = (2 * (-1 + 0.9 * torch.randn(B, 52, 384, generator=gen)) / 0.81).float().to(DEV)
+    w_cn = (0.5 + torch.rand(T, 42, generator=gen))[:, torch.as_tensor(g.chk)].contiguous().to(DEV)
+    w_vn = (0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV)
+    res = {}
+    for path in ("stream", "fused"):
+        cfg = DecodeCfg(kind=kind, qbit=5, vn_cumulative=True, path=path)
+        res[path] = decode(g, cfg, x, T, w_cn=w_cn, w_vn=w_vn)
+    assert torch.equal(res["stream"][0], res["fused"][0])
+    assert torch.equal(res["stream"][1], res["fused"][1])  # final c2v state
+
+
+def test_fast_path_selection():
+    import ctypes
+    from nldpc import _lib
+    from nldpc.decode import KIND_NEURAL, DecodeCfg
+    L = _lib.lib()
+    for bg, Z, want in ((BG2, 384, 1), (BG2, 16, 1), (WIMAX, 24, 1), (BG2, 64, 0)):
+        g = _graph(bg, Z)
+        for save, ucn, exp in ((0, False, want), (1, False, 0), (0, True, 0)):
+            cfg = DecodeCfg(KIND_NEURAL if not ucn else 1, ucn=ucn).c_struct(False)
+            out = ctypes.c_int32(-1)
+            _lib.check(L.nldpc_fast_path(g.handle(DEV), ctypes.byref(cfg), 4, 20, save, ctypes.byref(out)))
+            assert out.value == exp, (Z, save, ucn)
