@@ -2,18 +2,20 @@
 
 Design (DESIGN.md §Fused kernel): one workgroup decodes G codewords for all T iterations without
 touching HBM for message state.  The c2v messages of a codeword (E*Z floats, 302 KB for BG2 z=384)
-live in the REGISTERS of the threads that own their variable copies: thread (part p, codeword g,
-copy v) owns every edge of the columns of part p at copy v, so the variable-node update (sum of the
-others, sequential fp32 in ascending check row: the reference's sgemm order) is register-only code.
-The check-node update needs each row's messages at cyclically shifted copies, so per iteration the
-v2c messages go through LDS in row chunks: owners write a chunk, every thread runs the check
-nodes of its rows of that chunk in LDS (gather at (h + s) mod Z, update, scatter back to the same
-addresses), owners read the new c2v back.  HBM traffic per codeword: the channel LLRs (re-read
-from L2 every iteration) and the T posteriors the API returns.
+live in the REGISTERS of the threads that own their variable copies: the columns are split into P
+parts; thread (part p, codeword g, lane copy u) owns every edge of the columns of part p at the Q
+copies v = u + q*Z/Q, so the variable-node update (sum of the others, sequential fp32 in ascending
+check row: the reference's sgemm order) is register-only code.  The check-node update needs each
+row's messages at cyclically shifted copies, so per iteration the v2c messages go through LDS in row
+chunks: owners write a chunk, every thread runs the check nodes of its rows of that chunk in LDS
+(gather at (h + s) mod Z, update, scatter back to the same addresses), owners read the new c2v
+back.  Degree-1 columns keep no state at all (their v2c is the channel value; their c2v only feeds
+their own posterior, written as soon as it comes back).  HBM traffic per codeword: the channel LLRs
+(re-read from L2 every iteration) and the T posteriors the API returns.
 
 Everything that indexes registers is emitted as straight-line code with literal indices, so the
 generator needs the graph structure at build time; the per-edge arithmetic is the shared
-nldpc_node.h code (cn_core / cn_epilogue / vn_channel), identical to the streaming kernels.
+nldpc_node.h / nldpc_fused.h code, identical to the streaming kernels (tests compare both paths).
 
 Usage: python3 gen_fused.py OUT.hip RESOURCE_DIR
 """
@@ -22,50 +24,50 @@ import sys
 
 import numpy as np
 
+PARTS = [int(x) for x in filter(None, os.environ.get("NLDPC_GEN_PARTS", "").split(","))]  # debug
 SKIP = set(filter(None, os.environ.get("NLDPC_GEN_SKIP", "").split(",")))  # debug: drop phases
 LDS_BYTES = 160 * 1024 - 2048  # leave room for the compiler / alignment
 
-# (tag, base graph file, Z, codewords per workgroup G, parts P)
+# (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q)
 SPECS = [
-    ("bg2_z384", "basegraph2_set0.txt", 384, 1, 2),
-    ("bg2_z16", "basegraph2_set0.txt", 16, 16, 2),
-    ("wimax_z24", "wman_N0576_R34_z24.txt", 24, 16, 1),
+    ("bg2_z384", "basegraph2_set0.txt", 384, 1, 8, 3),
+    ("bg2_z16", "basegraph2_set0.txt", 16, 16, 2, 1),
+    ("wimax_z24", "wman_N0576_R34_z24.txt", 24, 16, 1, 1),
 ]
 
 
+def balance(items, weight, P):
+    """Greedy partition of items (heaviest first) into P bins of similar total weight."""
+    load = [0] * P
+    bins = [[] for _ in range(P)]
+    for it in sorted(items, key=lambda x: -weight(x)):
+        k = int(np.argmin(load))
+        bins[k].append(it)
+        load[k] += weight(it)
+    return [sorted(b) for b in bins]
+
+
 class Spec:
-    def __init__(self, tag, hb, Z, G, P):
-        self.tag, self.hb, self.Z, self.G, self.P = tag, hb, Z, G, P
+    def __init__(self, tag, hb, Z, G, P, Q):
+        assert Z % Q == 0
+        self.tag, self.hb, self.Z, self.G, self.P, self.Q = tag, hb, Z, G, P, Q
+        self.ZT = Z // Q
         self.M, self.N = hb.shape
         rows, cols = np.nonzero(hb != -1)
         self.E = len(rows)
-        self.chk, self.var = rows, cols
         self.shift = hb[rows, cols] % Z
-        self.row_edges = [list(np.nonzero(rows == i)[0]) for i in range(self.M)]
-        self.col_edges = [list(np.nonzero(cols == j)[0]) for j in range(self.N)]
-        dv = np.array([len(c) for c in self.col_edges])
-        # columns -> parts, balancing edges (owner registers)
-        load = [0] * P
-        self.part_cols = [[] for _ in range(P)]
-        for j in np.argsort(-dv, kind="stable"):
-            k = int(np.argmin(load))
-            self.part_cols[k].append(int(j))
-            load[k] += int(dv[j])
-        self.part_cols = [sorted(c) for c in self.part_cols]
-        # Degree-1 columns keep no register state: their v2c is the channel value alone and their
-        # c2v only enters their own posterior, which is written as soon as it is read back from LDS.
-        self.reg_cols = [[j for j in c if len(self.col_edges[j]) > 1] for c in self.part_cols]
-        self.d1_cols = [[j for j in c if len(self.col_edges[j]) == 1] for c in self.part_cols]
-        self.slots = []  # per part: register slot -> edge (column by column, ascending check row)
-        for p in range(P):
-            s = []
-            for j in self.reg_cols[p]:
-                s += [int(e) for e in self.col_edges[j]]
-            self.slots.append(s)
-        self.smax = max(1, max(len(s) for s in self.slots))
-        # row chunks: contiguous row ranges whose edges x Z x G fit in LDS
+        self.row_edges = [[int(e) for e in np.nonzero(rows == i)[0]] for i in range(self.M)]
+        self.col_edges = [[int(e) for e in np.nonzero(cols == j)[0]] for j in range(self.N)]
+        deg = lambda j: len(self.col_edges[j])  # noqa: E731
+        multi = [j for j in range(self.N) if deg(j) > 1]
+        single = [j for j in range(self.N) if deg(j) == 1]
+        self.reg_cols = balance(multi, deg, P)  # columns whose messages live in registers
+        self.d1_cols = balance(single, lambda j: 1, P)  # stateless degree-1 columns
+        self.slots = [[e for j in cols_ for e in self.col_edges[j]] for cols_ in self.reg_cols]
+        self.smax = max(1, max(len(s) for s in self.slots)) * Q
+        # row chunks: contiguous row ranges whose messages (edges x Z x G) fit in LDS
         cap = (LDS_BYTES // (4 * G) - 32) // Z
-        self.chunks = []  # list of (row_begin, row_end, edge_begin, edge_end)
+        self.chunks = []  # (row_begin, row_end, edge_begin, edge_end)
         r0 = 0
         while r0 < self.M:
             e0 = self.row_edges[r0][0]
@@ -79,191 +81,262 @@ class Spec:
         self.chunk_floats = max(e1 - e0 for _, _, e0, e1 in self.chunks) * Z
         if G > 1:  # codeword stride = 1 (mod 32 banks) so lanes of different codewords do not collide
             self.chunk_floats += (1 - self.chunk_floats) % 32
-        # check rows of every chunk -> parts, balancing sum of degrees
-        self.cn_rows = []
-        for (r0, r1, _, _) in self.chunks:
-            load = [0] * P
-            rp = [[] for _ in range(P)]
-            for i in sorted(range(r0, r1), key=lambda i: -len(self.row_edges[i])):
-                k = int(np.argmin(load))
-                rp[k].append(i)
-                load[k] += len(self.row_edges[i])
-            self.cn_rows.append([sorted(r) for r in rp])
-        self.threads = P * G * Z
-        assert self.threads <= 1024 and (G * Z) % 64 == 0, (tag, self.threads)
+        self.cn_rows = [balance(list(range(r0, r1)), lambda i: len(self.row_edges[i]), P)
+                        for (r0, r1, _, _) in self.chunks]
+        self.lanes = G * self.ZT  # threads per part
+        self.threads = P * self.lanes
+        assert self.threads <= 1024 and self.lanes % 64 == 0, (tag, self.threads)
         self.max_dc = max(len(r) for r in self.row_edges)
 
-    def chunk_of(self, e):
-        for c, (_, _, e0, e1) in enumerate(self.chunks):
-            if e0 <= e < e1:
-                return c
-        raise KeyError(e)
 
-
-def emit(spec: Spec) -> str:
-    S, Z, G = spec, spec.Z, spec.G
+def emit(S: Spec) -> str:
+    Z, G, Q, ZT, NZ = S.Z, S.G, S.Q, S.ZT, S.N * S.Z
     L = []
     w = L.append
     CF = S.chunk_floats
-    w(f"// ---- {S.tag}: M={S.M} N={S.N} E={S.E} Z={Z}, {G} codeword(s) x {S.P} part(s) x {Z} copies = "
-      f"{S.threads} threads; slots/part {[len(s) for s in S.slots]}; "
-      f"{len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B")
+    w(f"// ---- {S.tag}: M={S.M} N={S.N} E={S.E} Z={Z}; workgroup = {G} codeword(s) x {S.P} part(s) x {ZT} lanes "
+      f"= {S.threads} threads, {Q} cop{'y' if Q == 1 else 'ies'} per lane; register slots/part "
+      f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B")
     w(f"namespace fused_{S.tag} {{")
-    w(f"constexpr int Z = {Z}, G = {G}, N = {S.N}, E = {S.E}, SMAX = {S.smax}, CHF = {CF};")
-    # VN (+ posterior of the previous iteration) per part, and the final posterior pass
+    w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E}, SMAX = {S.smax};")
+
+    def sl(p, q, k):  # register slot of copy q, part-slot k
+        return q * len(S.slots[p]) + k
+
+    # ---------------------------------------------------------------- variable nodes
+    # global accesses: bload/bstore(descriptor, lane byte offset vo, constant byte offset)
+    def X(j, q):  # byte offset of variable copy (column j, lane copy q) in a [N][Z] codeword
+        return 4 * (j * Z + q * ZT)
+
     for p in range(S.P):
         cols = S.reg_cols[p]
-        if not cols:
-            for final in (False, True):
-                w("template <int KIND>")
-                w(f"__device__ __forceinline__ void {'post' if final else 'vn'}_p{p}(float (&)[SMAX], const FusedArgs&, "
-                  f"const float*, int, int, float*, bool) {{}}")
-            continue
         for final in (False, True):
-            w("template <int KIND>")
             fname = f"post_p{p}" if final else f"vn_p{p}"
-            w(f"__device__ __forceinline__ void {fname}(float (&c)[SMAX], const FusedArgs& a, const float* __restrict__ xb, "
-              f"int lo, int it, float* __restrict__ post, bool live) {{")
-            w("    asm volatile(\"\" : \"+v\"(lo));  // recompute per-column offsets every iteration (no hoisting)")
+            w("template <int KIND>")
+            w(f"__device__ __forceinline__ void {fname}(float (&c)[SMAX], const FusedArgs& a, rsrc_t xr, uint32_t vo, "
+              f"int it, rsrc_t pr) {{")
+            if not cols:
+                w("}")
+                continue
+            # channel values of the next column are loaded one column ahead; a scheduling barrier
+            # between columns keeps the compiler from hoisting every load (and register) to the top
+            for q in range(Q):
+                w(f"    float xn{q} = bload(xr, vo, {X(cols[0], q)});")
             s = 0
-            # channel values are software-pipelined one column ahead; a scheduling barrier between
-            # columns keeps the compiler from hoisting every load (and its register) to the top
-            w(f"    float xnext = xb[lo + {cols[0] * Z}];")
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
                 w(f"    {{  // column {j}, degree {d}")
-                w("        const float xav = xnext;")
+                for q in range(Q):
+                    w(f"        const float xa{q} = xn{q};")
                 if n + 1 < len(cols):
-                    w(f"        xnext = xb[lo + {cols[n + 1] * Z}];")
-                w("        float P = 0.f;")
-                if not final:
-                    w(f"        const float x0 = fadd(0.f, vn_channel<KIND>(xav, a.w_vn, N, {j}, a.vn_prefix + it + 1, a.qbit));")
-                    for k in range(d):
-                        expr = "P"
-                        for m in range(k + 1, d):
-                            expr = f"fadd({expr}, c[{s + m}])"
-                        w(f"        {{ const float S_ = {expr}; P = fadd(P, c[{s + k}]); c[{s + k}] = fadd(x0, S_); }}")
-                else:
-                    for k in range(d):
-                        w(f"        P = fadd(P, c[{s + k}]);")
-                w(f"        if (post && live) post[lo + {j * Z}] = posterior<KIND>(xav, P, a);")
+                    for q in range(Q):
+                        w(f"        xn{q} = bload(xr, vo, {X(cols[n + 1], q)});")
+                for q in range(Q):
+                    w(f"        float P{q} = 0.f;")
+                    if not final:
+                        w(f"        const float x0_{q} = fadd(0.f, vn_channel<KIND>(xa{q}, a.w_vn, N, {j}, "
+                          f"a.vn_prefix + it + 1, a.qbit));")
+                        for k in range(d):
+                            expr = f"P{q}"
+                            for m in range(k + 1, d):
+                                expr = f"fadd({expr}, c[{sl(p, q, s + m)}])"
+                            # one edge at a time: the fake dependence of the running prefix on the new
+                            # message keeps the compiler from running the prefix chain ahead and holding
+                            # every partial sum in a register (dependent VALU ops issue back to back anyway)
+                            w(f"        {{ const float S_ = {expr}; const float o_ = c[{sl(p, q, s + k)}]; "
+                              f"c[{sl(p, q, s + k)}] = fadd(x0_{q}, S_); "
+                              f"asm volatile(\"\" : \"+v\"(P{q}) : \"v\"(c[{sl(p, q, s + k)}])); P{q} = fadd(P{q}, o_); }}")
+                    else:
+                        for k in range(d):
+                            w(f"        P{q} = fadd(P{q}, c[{sl(p, q, s + k)}]);")
+                    w(f"        bstore(pr, vo, {X(j, q)}, posterior<KIND>(xa{q}, P{q}, a));")
+                    if q + 1 < Q:
+                        w("        __builtin_amdgcn_sched_barrier(0);  // one copy's chains at a time")
                 w("    }")
                 w("    __builtin_amdgcn_sched_barrier(0);")
                 s += d
             w("}")
-    # chunk writes / reads per part
+
+    # ---------------------------------------------------------------- LDS chunk write / read-back
+    def own(e, q, e0):
+        """LDS index (expression in u) where the owner of variable copy u + q*ZT puts edge e's message:
+        check copy h = (v - s_e) mod Z of the chunk's check-ordered image.  Only one of the Q copies
+        of a shifted edge can wrap inside the lane range; the others are a constant offset."""
+        cq = (q * ZT - int(S.shift[e])) % Z
+        base = (e - e0) * Z + cq
+        if cq + ZT <= Z:
+            return f"{base} + u"
+        return f"{base} + u - (u >= {Z - cq} ? {Z} : 0)"
+
     for p in range(S.P):
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
-            sl = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
-            d1 = [(j, int(S.col_edges[j][0])) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
+            mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
+            d1 = [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
+            # degree-1 columns: their channel values are loaded in one batch up front (one memory
+            # latency per phase), then combined and written / turned into posteriors
             w("template <int KIND>")
-            w(f"__device__ __forceinline__ void wr_p{p}_c{ci}(const float (&c)[SMAX], float* lds, int v, const FusedArgs& a, "
-              f"const float* __restrict__ xb, int lo, int it) {{")
-            w("    asm volatile(\"\" : \"+v\"(v));")
-            w("    asm volatile(\"\" : \"+v\"(lo));")
-            for k, e in sl:
-                w(f"    lds[{(e - e0) * Z} + v] = c[{k}];")
+            w(f"__device__ __forceinline__ void wr_p{p}_c{ci}(const float (&c)[SMAX], float* lds, int u, "
+              f"const FusedArgs& a, rsrc_t xr, uint32_t vo, int it) {{")
+            w("    asm volatile(\"\" : \"+v\"(u));  // LDS addresses are recomputed here, not hoisted out of the loop")
+            for n, (j, e) in enumerate(d1):
+                for q in range(Q):
+                    w(f"    const float x{n}_{q} = bload(xr, vo, {X(j, q)});")
+            for q in range(Q):
+                for k, e in mine:
+                    w(f"    lds[{own(e, q, e0)}] = c[{sl(p, q, k)}];")
             for n, (j, e) in enumerate(d1):  # v2c = (0 + xin) + 0: no other edge in the column
-                w(f"    lds[{(e - e0) * Z} + v] = fadd(fadd(0.f, vn_channel<KIND>(xb[lo + {j * Z}], a.w_vn, N, {j}, "
-                  f"a.vn_prefix + it + 1, a.qbit)), 0.f);")
-                if n % 4 == 3:
-                    w("    __builtin_amdgcn_sched_barrier(0);")
+                for q in range(Q):
+                    w(f"    lds[{own(e, q, e0)}] = fadd(fadd(0.f, vn_channel<KIND>(x{n}_{q}, "
+                      f"a.w_vn, N, {j}, a.vn_prefix + it + 1, a.qbit)), 0.f);")
             w("}")
             w("template <int KIND>")
-            w(f"__device__ __forceinline__ void rd_p{p}_c{ci}(float (&c)[SMAX], const float* lds, int v, const FusedArgs& a, "
-              f"const float* __restrict__ xb, int lo, float* __restrict__ post, float* __restrict__ co, bool live) {{")
-            w("    asm volatile(\"\" : \"+v\"(v));")
-            w("    asm volatile(\"\" : \"+v\"(lo));")
-            for k, e in sl:
-                w(f"    c[{k}] = lds[{(e - e0) * Z} + v];")
-            for n, (j, e) in enumerate(d1):  # posterior of this iteration right away (and the final state if asked)
-                if n % 4 == 0:
-                    w("    __builtin_amdgcn_sched_barrier(0);")
-                w("    {")
-                w(f"        const float c_ = lds[{(e - e0) * Z} + v];")
-                w(f"        if (post && live) post[lo + {j * Z}] = posterior<KIND>(xb[lo + {j * Z}], fadd(0.f, c_), a);")
-                w(f"        if (co && live) co[{e * Z}] = c_;")
+            w(f"__device__ __forceinline__ void rd_p{p}_c{ci}(float (&c)[SMAX], const float* lds, int u, "
+              f"const FusedArgs& a, rsrc_t xr, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co) {{")
+            w("    asm volatile(\"\" : \"+v\"(u));")
+            for n, (j, e) in enumerate(d1):
+                for q in range(Q):
+                    w(f"    const float x{n}_{q} = bload(xr, vo, {X(j, q)});")
+            for q in range(Q):
+                for k, e in mine:
+                    w(f"    c[{sl(p, q, k)}] = lds[{own(e, q, e0)}];")
+            for n, (j, e) in enumerate(d1):  # this iteration's posterior right away
+                for q in range(Q):
+                    w(f"    bstore(pr, vo, {X(j, q)}, posterior<KIND>(x{n}_{q}, fadd(0.f, lds[{own(e, q, e0)}]), a));")
+            if d1:
+                w("    if (has_co) {  // final message state (last iteration only)")
+                for n, (j, e) in enumerate(d1):
+                    for q in range(Q):
+                        w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, lds[{own(e, q, e0)}]);")
                 w("    }")
             w("}")
-    # check nodes per part per chunk
+
+    # ---------------------------------------------------------------- check nodes (table driven)
+    # LDS holds each edge's Z messages in CHECK order (the owners rotate on write/read-back), so the
+    # thread of check copy h reads every edge of its row at h: one address per row, the edges at
+    # immediate offsets k*Z.  Rows are grouped by degree so every loop has a compile-time degree.
+    tab, groups = [], {}
     for p in range(S.P):
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
-            w("template <int KIND>")
-            w(f"__device__ __forceinline__ void cn_p{p}_c{ci}(float* lds, int h, const FusedArgs& a, int it) {{")
-            w("    asm volatile(\"\" : \"+v\"(h));")
-            w("    const float* wc = a.w_cn ? a.w_cn + (int64_t)it * E : nullptr;")
-            w("    const float* bs = a.bias ? a.bias + (int64_t)it * E : nullptr;")
-            for i in S.cn_rows[ci][p]:
-                es = S.row_edges[i]
-                d = len(es)
-                w(f"    {{  // check row {i}, degree {d}")
-                w(f"        int ad[{d}];")
-                w(f"        float m[{d}];")
-                for k, e in enumerate(es):
-                    sft = int(S.shift[e])
-                    base = (e - e0) * Z
-                    if sft == 0:
-                        w(f"        ad[{k}] = {base} + h;")
-                    else:
-                        w(f"        {{ const int t_ = h + {sft}; ad[{k}] = {base} + (t_ >= Z ? t_ - Z : t_); }}")
-                    w(f"        m[{k}] = lds[ad[{k}]];")
-                w(f"        CnCore<{d}> core;")
-                w(f"        cn_core<{d}, KIND>(m, {d}, a.qbit, a.lo, a.hi, core);")
-                for k, e in enumerate(es):
-                    w(f"        lds[ad[{k}]] = cn_epilogue<KIND, false>(core.out0[{k}], wc ? wc[{e}] : 1.f, 0.f, "
-                      f"bs ? bs[{e}] : 0.f, 0.f, wc != nullptr, false, a.qbit, a.lo, a.hi).c;")
-                w("    }")
-                w("    __builtin_amdgcn_sched_barrier(0);")
-            w("}")
-    # the kernel
+            gl = []
+            rows = S.cn_rows[ci][p]
+            for dc in sorted({len(S.row_edges[i]) for i in rows}, reverse=True):
+                sel = [i for i in rows if len(S.row_edges[i]) == dc]
+                gl.append((dc, len(tab), len(sel)))
+                tab += [S.row_edges[i][0] for i in sel]
+            groups[(p, ci)] = gl
+    S.cn_groups = groups
+    w(f"__constant__ int32_t cn_tab[{max(1, len(tab))}] = {{{', '.join(str(x) for x in tab) or '0'}}};")
+    w("template <int KIND, int DC>")
+    w("__device__ __forceinline__ void cn_rows(float* lds, int u, const FusedArgs& a, int it, int t0, int n, int e0c) {")
+    w("    asm volatile(\"\" : \"+v\"(u));")
+    w("    for (int r = 0; r < n; ++r) {")
+    w("        const int e0 = cn_tab[t0 + r];  // first edge of the row (its edges are consecutive)")
+    w("        float* rp = lds + (e0 - e0c) * Z + u;")
+    w("        float wv[DC], bv[DC];")
+    w("        const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + e0) : nullptr;")
+    w("        const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + e0) : nullptr;")
+    w("        // whole-row scalar loads (one uniform test per row, not per edge, so the loads can merge)")
+    w("        if (KIND == NLDPC_NEURAL || wc) {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) wv[k] = wc[k];")
+    w("        } else {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) wv[k] = 1.f;")
+    w("        }")
+    w("        if (KIND == NLDPC_NEURAL || bs) {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) bv[k] = bs[k];")
+    w("        } else {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) bv[k] = 0.f;")
+    w("        }")
+    w("#pragma unroll")
+    w(f"        for (int q = 0; q < {Q}; ++q) {{  // one check copy at a time: the state owns the registers")
+    w("            float m[DC];")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) m[k] = rp[k * Z + q * ZT];")
+    w("            if (KIND == NLDPC_NEURAL) {")
+    w("                neural_row<DC>(m, wv, bv);")
+    w("            } else {")
+    w("                CnCore<DC> core;")
+    w("                cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core);")
+    w("#pragma unroll")
+    w("                for (int k = 0; k < DC; ++k)")
+    w("                    m[k] = cn_epilogue<KIND, false>(core.out0[k], wv[k], 0.f, 0.f, 0.f, wc != nullptr, false, a.qbit,"
+      " a.lo, a.hi).c;")
+    w("            }")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) rp[k * Z + q * ZT] = m[k];")
+    if Q > 1:
+        w("            __builtin_amdgcn_sched_barrier(0);")
+    w("        }")
+    w("    }")
+    w("}")
+
+    # ---------------------------------------------------------------- the kernel
+    def each_part(fmt, indent="        "):
+        for p in PARTS or range(S.P):
+            w(f"{indent}{'if' if p == 0 else 'else if'} (p == {p}) {fmt.format(p=p)};")
+
+    # Each part runs its own copy of the whole iteration loop: its register state never meets another
+    # part's at a control-flow join (per-phase part branches inside one loop made the register
+    # allocator insert phi copies and spill).  The parts still meet at every s_barrier: a hardware
+    # barrier counts waves, not program counters, and every part executes the same barrier sequence.
+    for p in range(S.P):
+        if PARTS and p not in PARTS:
+            continue
+        w("template <int KIND>")
+        w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
+          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc) {{")
+        w(f"    float c[SMAX];")
+        w("#pragma unroll")
+        w("    for (int k = 0; k < SMAX; ++k) c[k] = 0.f;")
+        w("    for (int it = 0; it < a.T; ++it) {")
+        w("        const float* pp = it >= 1 ? a.outs.p[it - 1] : nullptr;  // previous iteration's posterior")
+        w(f"        const rsrc_t pr = make_rsrc(pp ? pp + blk * {NZ} : a.xa, pp ? nlive * {4 * NZ} : 0);  // no output: stores dropped")
+        if "vn" not in SKIP:
+            w(f"        vn_p{p}<KIND>(c, a, xr, vo, it, pr);")
+        w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
+        w(f"        const rsrc_t nr = make_rsrc(pn ? pn + blk * {NZ} : a.xa, pn ? nlive * {4 * NZ} : 0);")
+        w("        const bool co_last = a.c2v_out && it == a.T - 1;")
+        for ci in range(len(S.chunks)):
+            w(f"        wr_p{p}_c{ci}<KIND>(c, lds, u, a, xr, vo, it);")
+            w("        __syncthreads();")
+            if "cn" not in SKIP:
+                for dc, t0, n in S.cn_groups[(p, ci)]:
+                    w(f"        cn_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]});")
+            w("        __syncthreads();")
+            w(f"        rd_p{p}_c{ci}<KIND>(c, lds, u, a, xr, vo, nr, cr, vc, co_last);")
+            w("        __syncthreads();")
+        w("    }")
+        w("    const float* pl = a.outs.p[a.T - 1];")
+        w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
+        w(f"    post_p{p}<KIND>(c, a, xr, vo, a.T, lr);")
+        w("    if (a.c2v_out) {")
+        for q in range(Q):
+            for k, e in enumerate(S.slots[p]):
+                w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, c[{sl(p, q, k)}]);")
+        w("    }")
+        w("}")
     w("template <int KIND>")
     w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void kernel(FusedArgs a) {{")
     w(f"    __shared__ float lds_all[{CF * G}];")
     w("    const int t = threadIdx.x;")
-    w(f"    // every wave lies in one part ({G * Z} threads per part): make the part wave-uniform so the")
-    w(f"    // per-part code is a scalar branch (a divergent one would keep two copies of the state alive)")
-    w(f"    const int p = __builtin_amdgcn_readfirstlane(t / ({G * Z}));")
-    w(f"    const int r = t - p * {G * Z};")
-    w(f"    const int g = r / {Z};")
-    w(f"    const int v = r - g * {Z};")
-    w("    const int64_t blk = (int64_t)blockIdx.x * G;  // first codeword of the workgroup")
-    w("    const bool live = blk + g < a.B;")
-    w(f"    const int lo = (live ? g : (int)(a.B - 1 - blk)) * {S.N * Z} + v;  // lane offset in the block's codewords")
-    w(f"    const float* __restrict__ xb = a.xa + blk * {S.N * Z};")
+    w(f"    // every wave lies in one part ({S.lanes} threads per part): the part is wave-uniform")
+    w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes});")
+    w(f"    const int r = t - p * {S.lanes};")
+    w(f"    const int g = r / {ZT};")
+    w(f"    const int u = r - g * {ZT};")
+    w(f"    const int64_t blk = (int64_t)blockIdx.x * {G};  // first codeword of the workgroup")
+    w(f"    const int nlive = a.B - blk < {G} ? (int)(a.B - blk) : {G};")
+    w("    // lane byte offsets into the block's codewords; a lane past the last codeword gets an offset")
+    w("    // beyond every descriptor's range (its loads read 0, its stores are dropped)")
+    w(f"    const uint32_t vo = g < nlive ? 4u * (g * {NZ} + u) : 0x80000000u;  // [N][Z] layouts")
+    w(f"    const uint32_t vc = g < nlive ? 4u * (g * {S.E * Z} + u) : 0x80000000u;  // [E][Z] c2v state")
+    w(f"    const rsrc_t xr = make_rsrc(a.xa + blk * {NZ}, nlive * {4 * NZ});")
+    w(f"    const rsrc_t cr = make_rsrc(a.c2v_out ? a.c2v_out + blk * {S.E * Z} : a.xa, nlive * {4 * S.E * Z});")
     w(f"    float* lds = lds_all + g * {CF};")
-    w("    float c[SMAX];")
-    w("#pragma unroll")
-    w("    for (int k = 0; k < SMAX; ++k) c[k] = 0.f;")
-    w("    for (int it = 0; it < a.T; ++it) {")
-    w(f"        float* post = (it >= 1 && a.outs.p[it - 1]) ? a.outs.p[it - 1] + blk * {S.N * Z} : nullptr;")
-    for p in range(S.P):
-        if "vn" not in SKIP:
-            w(f"        {'if' if p == 0 else 'else if'} (p == {p}) vn_p{p}<KIND>(c, a, xb, lo, it, post, live);")
-    w(f"        float* post_now = a.outs.p[it] ? a.outs.p[it] + blk * {S.N * Z} : nullptr;  // degree-1 columns")
-    w("        float* co_last = (a.c2v_out && it == a.T - 1) ? a.c2v_out + (blk + g) * (int64_t)(E * Z) + v : nullptr;")
-    for ci in range(len(S.chunks)):
-        for p in range(S.P):
-            w(f"        {'if' if p == 0 else 'else if'} (p == {p}) wr_p{p}_c{ci}<KIND>(c, lds, v, a, xb, lo, it);")
-        w("        __syncthreads();")
-        for p in range(S.P):
-            if "cn" not in SKIP:
-                w(f"        {'if' if p == 0 else 'else if'} (p == {p}) cn_p{p}_c{ci}<KIND>(lds, v, a, it);")
-        w("        __syncthreads();")
-        for p in range(S.P):
-            w(f"        {'if' if p == 0 else 'else if'} (p == {p}) rd_p{p}_c{ci}<KIND>(c, lds, v, a, xb, lo, post_now, co_last, live);")
-        w("        __syncthreads();")
-    w("    }")
-    w(f"    float* post = a.outs.p[a.T - 1] ? a.outs.p[a.T - 1] + blk * {S.N * Z} : nullptr;")
-    for p in range(S.P):
-        w(f"    {'if' if p == 0 else 'else if'} (p == {p}) post_p{p}<KIND>(c, a, xb, lo, a.T, post, live);")
-    w("    if (a.c2v_out && live) {")
-    w("        float* co = a.c2v_out + (blk + g) * (int64_t)(E * Z) + v;")
-    for p in range(S.P):
-        w(f"        {'if' if p == 0 else 'else if'} (p == {p}) {{")
-        for k, e in enumerate(S.slots[p]):
-            w(f"            co[{e * Z}] = c[{k}];")
-        w("        }")
-    w("    }")
+    each_part("run_p{p}<KIND>(a, lds, u, blk, nlive, xr, vo, cr, vc)", indent="    ")
     w("}")
     w(f"static const int32_t basegraph[{S.M * S.N}] = {{{', '.join(str(int(x)) for x in S.hb.reshape(-1))}}};")
     w("}  // namespace")
@@ -273,9 +346,12 @@ def emit(spec: Spec) -> str:
 def main():
     out, res = sys.argv[1], sys.argv[2]
     specs = []
-    for tag, fname, Z, G, P in SPECS:
+    only = set(filter(None, os.environ.get("NLDPC_GEN_ONLY", "").split(",")))  # debug: subset of specs
+    for tag, fname, Z, G, P, Q in SPECS:
+        if only and tag not in only:
+            continue
         hb = np.loadtxt(os.path.join(res, fname), int, delimiter="\t")
-        specs.append(Spec(tag, hb, Z, G, P))
+        specs.append(Spec(tag, hb, Z, G, P, Q))
     src = [
         "// GENERATED by gen_fused.py from the base graphs in resources/ -- do not edit.",
         "#include <hip/hip_runtime.h>",
@@ -285,9 +361,14 @@ def main():
     for s in specs:
         src.append(emit(s))
     src.append("template <int KIND> static void* pick(int i) {")
+    kinds = os.environ.get("NLDPC_GEN_KINDS")  # debug: instantiate a subset of kinds
+    if kinds:
+        src.append(f"    if constexpr ({' && '.join(f'KIND != {k}' for k in kinds.split(','))}) return nullptr; else {{")
     for i, s in enumerate(specs):
         src.append(f"    if (i == {i}) return reinterpret_cast<void*>(&fused_{s.tag}::kernel<KIND>);")
     src.append("    return nullptr;")
+    if kinds:
+        src.append("    }")
     src.append("}")
     src.append("const FusedSpec* fused_specs(int* n) {")
     src.append(f"    static const FusedSpec tab[{len(specs)}] = {{")
