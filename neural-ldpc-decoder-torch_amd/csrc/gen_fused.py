@@ -98,62 +98,104 @@ def emit(S: Spec) -> str:
       f"= {S.threads} threads, {Q} cop{'y' if Q == 1 else 'ies'} per lane; register slots/part "
       f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B")
     w(f"namespace fused_{S.tag} {{")
-    w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E}, SMAX = {S.smax};")
+    w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E};")
 
-    def sl(p, q, k):  # register slot of copy q, part-slot k
-        return q * len(S.slots[p]) + k
+    # Register state of part p: copies are paired (q = 0,1 / 2,3 ...) into float2 arrays so the VN's
+    # additions run as packed fp32 (v_pk_add_f32: two IEEE adds per lane, same rounding); an odd
+    # copy count leaves one scalar array.  The channel values a thread needs every iteration are
+    # loaded once into registers (xp*/xs for its register columns, xd for its degree-1 columns).
+    NPAIR, SINGLE = Q // 2, Q % 2
+
+    def ref(q, k):
+        if q < 2 * NPAIR:
+            return f"cp{q // 2}[{k}].{'x' if q % 2 == 0 else 'y'}"
+        return f"cs[{k}]"
+
+    def xref(p, j, q):
+        cols = S.reg_cols[p]
+        if j in cols:
+            n = cols.index(j)
+            return f"xp{q // 2}[{n}].{'x' if q % 2 == 0 else 'y'}" if q < 2 * NPAIR else f"xs[{n}]"
+        n = S.d1_cols[p].index(j)
+        return f"xd[{n * Q + q}]"
+
+    def state_params(p, const=False):
+        sp = len(S.slots[p])
+        c = "const " if const else ""
+        ps = [f"{c}f2 (&cp{i})[{max(sp, 1)}]" for i in range(NPAIR)]
+        if SINGLE:
+            ps.append(f"{c}float (&cs)[{max(sp, 1)}]")
+        return ", ".join(ps)
+
+    def state_args():
+        return ", ".join([f"cp{i}" for i in range(NPAIR)] + (["cs"] if SINGLE else []))
+
+    def x_params(p):
+        nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
+        ps = [f"const f2 (&xp{i})[{nr}]" for i in range(NPAIR)]
+        if SINGLE:
+            ps.append(f"const float (&xs)[{nr}]")
+        ps.append(f"const float (&xd)[{nd}]")
+        return ", ".join(ps)
+
+    def x_args():
+        return ", ".join([f"xp{i}" for i in range(NPAIR)] + (["xs"] if SINGLE else []) + ["xd"])
 
     # ---------------------------------------------------------------- variable nodes
     # global accesses: bload/bstore(descriptor, lane byte offset vo, constant byte offset)
     def X(j, q):  # byte offset of variable copy (column j, lane copy q) in a [N][Z] codeword
         return 4 * (j * Z + q * ZT)
 
+    def vn_group(p, n, j, s, d, final, vec, names, xin):
+        """VN (or final posterior) of column j (n-th register column of part p) for one copy group:
+        vec: float2 pair (names = ('cp0', 'x'/'y' copies)) or scalar."""
+        T_ = "f2" if vec else "float"
+        arr = names
+        c = lambda k: f"{arr}[{s + k}]"  # noqa: E731
+        add = (lambda x, y: f"({x} + {y})") if vec else (lambda x, y: f"fadd({x}, {y})")  # noqa: E731
+        zero = "f2{0.f, 0.f}" if vec else "0.f"
+        w(f"        {{  // column {j}, degree {d}, {'copies ' + xin if vec else 'copy ' + xin}")
+        w(f"            {T_} P = {zero};")
+        if not final:
+            ch = (f"vn_channel2<KIND>({xin}, a.w_vn, N, {j}, a.vn_prefix + it + 1, a.qbit)" if vec else
+                  f"vn_channel<KIND>({xin}, a.w_vn, N, {j}, a.vn_prefix + it + 1, a.qbit)")
+            w(f"            const {T_} x0 = {add(zero, ch)};")
+            for k in range(d):
+                expr = "P"
+                for m in range(k + 1, d):
+                    expr = add(expr, c(m))
+                # one edge at a time: the fake dependence of the running prefix on the new message
+                # keeps the compiler from running the prefix chain ahead and holding every partial
+                # sum in a register (dependent VALU ops issue back to back anyway)
+                w(f"            {{ const {T_} S_ = {expr}; const {T_} o_ = {c(k)}; {c(k)} = {add('x0', 'S_')}; "
+                  f"asm volatile(\"\" : \"+v\"(P) : \"v\"({c(k)})); P = {add('P', 'o_')}; }}")
+        else:
+            for k in range(d):
+                w(f"            P = {add('P', c(k))};")
+        return T_
+
     for p in range(S.P):
         cols = S.reg_cols[p]
         for final in (False, True):
             fname = f"post_p{p}" if final else f"vn_p{p}"
             w("template <int KIND>")
-            w(f"__device__ __forceinline__ void {fname}(float (&c)[SMAX], const FusedArgs& a, rsrc_t xr, uint32_t vo, "
-              f"int it, rsrc_t pr) {{")
-            if not cols:
-                w("}")
-                continue
-            # channel values of the next column are loaded one column ahead; a scheduling barrier
-            # between columns keeps the compiler from hoisting every load (and register) to the top
-            for q in range(Q):
-                w(f"    float xn{q} = bload(xr, vo, {X(cols[0], q)});")
+            w(f"__device__ __forceinline__ void {fname}({state_params(p)}, {x_params(p)}, const FusedArgs& a, "
+              f"uint32_t vo, int it, rsrc_t pr) {{")
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
-                w(f"    {{  // column {j}, degree {d}")
-                for q in range(Q):
-                    w(f"        const float xa{q} = xn{q};")
-                if n + 1 < len(cols):
-                    for q in range(Q):
-                        w(f"        xn{q} = bload(xr, vo, {X(cols[n + 1], q)});")
-                for q in range(Q):
-                    w(f"        float P{q} = 0.f;")
-                    if not final:
-                        w(f"        const float x0_{q} = fadd(0.f, vn_channel<KIND>(xa{q}, a.w_vn, N, {j}, "
-                          f"a.vn_prefix + it + 1, a.qbit));")
-                        for k in range(d):
-                            expr = f"P{q}"
-                            for m in range(k + 1, d):
-                                expr = f"fadd({expr}, c[{sl(p, q, s + m)}])"
-                            # one edge at a time: the fake dependence of the running prefix on the new
-                            # message keeps the compiler from running the prefix chain ahead and holding
-                            # every partial sum in a register (dependent VALU ops issue back to back anyway)
-                            w(f"        {{ const float S_ = {expr}; const float o_ = c[{sl(p, q, s + k)}]; "
-                              f"c[{sl(p, q, s + k)}] = fadd(x0_{q}, S_); "
-                              f"asm volatile(\"\" : \"+v\"(P{q}) : \"v\"(c[{sl(p, q, s + k)}])); P{q} = fadd(P{q}, o_); }}")
-                    else:
-                        for k in range(d):
-                            w(f"        P{q} = fadd(P{q}, c[{sl(p, q, s + k)}]);")
-                    w(f"        bstore(pr, vo, {X(j, q)}, posterior<KIND>(xa{q}, P{q}, a));")
-                    if q + 1 < Q:
-                        w("        __builtin_amdgcn_sched_barrier(0);  // one copy's chains at a time")
-                w("    }")
-                w("    __builtin_amdgcn_sched_barrier(0);")
+                for i in range(NPAIR):
+                    vn_group(p, n, j, s, d, final, True, f"cp{i}", f"xp{i}[{n}]")
+                    w(f"            const f2 y_ = posterior2<KIND>(xp{i}[{n}], P, a);")
+                    w(f"            bstore(pr, vo, {X(j, 2 * i)}, y_.x);")
+                    w(f"            bstore(pr, vo, {X(j, 2 * i + 1)}, y_.y);")
+                    w("        }")
+                    w("        __builtin_amdgcn_sched_barrier(0);")
+                if SINGLE:
+                    vn_group(p, n, j, s, d, final, False, "cs", f"xs[{n}]")
+                    w(f"            bstore(pr, vo, {X(j, Q - 1)}, posterior<KIND>(xs[{n}], P, a));")
+                    w("        }")
+                    w("        __builtin_amdgcn_sched_barrier(0);")
                 s += d
             w("}")
 
@@ -172,39 +214,31 @@ def emit(S: Spec) -> str:
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
             mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
             d1 = [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
-            # degree-1 columns: their channel values are loaded in one batch up front (one memory
-            # latency per phase), then combined and written / turned into posteriors
             w("template <int KIND>")
-            w(f"__device__ __forceinline__ void wr_p{p}_c{ci}(const float (&c)[SMAX], float* lds, int u, "
-              f"const FusedArgs& a, rsrc_t xr, uint32_t vo, int it) {{")
+            w(f"__device__ __forceinline__ void wr_p{p}_c{ci}({state_params(p, True)}, {x_params(p)}, float* lds, "
+              f"int u, const FusedArgs& a, int it) {{")
             w("    asm volatile(\"\" : \"+v\"(u));  // LDS addresses are recomputed here, not hoisted out of the loop")
-            for n, (j, e) in enumerate(d1):
-                for q in range(Q):
-                    w(f"    const float x{n}_{q} = bload(xr, vo, {X(j, q)});")
             for q in range(Q):
                 for k, e in mine:
-                    w(f"    lds[{own(e, q, e0)}] = c[{sl(p, q, k)}];")
-            for n, (j, e) in enumerate(d1):  # v2c = (0 + xin) + 0: no other edge in the column
+                    w(f"    lds[{own(e, q, e0)}] = {ref(q, k)};")
+            for j, e in d1:  # v2c = (0 + xin) + 0: no other edge in the column
                 for q in range(Q):
-                    w(f"    lds[{own(e, q, e0)}] = fadd(fadd(0.f, vn_channel<KIND>(x{n}_{q}, "
+                    w(f"    lds[{own(e, q, e0)}] = fadd(fadd(0.f, vn_channel<KIND>({xref(p, j, q)}, "
                       f"a.w_vn, N, {j}, a.vn_prefix + it + 1, a.qbit)), 0.f);")
             w("}")
             w("template <int KIND>")
-            w(f"__device__ __forceinline__ void rd_p{p}_c{ci}(float (&c)[SMAX], const float* lds, int u, "
-              f"const FusedArgs& a, rsrc_t xr, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co) {{")
+            w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
+              f"int u, const FusedArgs& a, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
-            for n, (j, e) in enumerate(d1):
-                for q in range(Q):
-                    w(f"    const float x{n}_{q} = bload(xr, vo, {X(j, q)});")
             for q in range(Q):
                 for k, e in mine:
-                    w(f"    c[{sl(p, q, k)}] = lds[{own(e, q, e0)}];")
-            for n, (j, e) in enumerate(d1):  # this iteration's posterior right away
+                    w(f"    {ref(q, k)} = lds[{own(e, q, e0)}];")
+            for j, e in d1:  # this iteration's posterior right away
                 for q in range(Q):
-                    w(f"    bstore(pr, vo, {X(j, q)}, posterior<KIND>(x{n}_{q}, fadd(0.f, lds[{own(e, q, e0)}]), a));")
+                    w(f"    bstore(pr, vo, {X(j, q)}, posterior<KIND>({xref(p, j, q)}, fadd(0.f, lds[{own(e, q, e0)}]), a));")
             if d1:
                 w("    if (has_co) {  // final message state (last iteration only)")
-                for n, (j, e) in enumerate(d1):
+                for j, e in d1:
                     for q in range(Q):
                         w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, lds[{own(e, q, e0)}]);")
                 w("    }")
@@ -285,37 +319,57 @@ def emit(S: Spec) -> str:
     for p in range(S.P):
         if PARTS and p not in PARTS:
             continue
+        sp = max(len(S.slots[p]), 1)
+        nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
         w("template <int KIND>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc) {{")
-        w(f"    float c[SMAX];")
+        for i in range(NPAIR):
+            w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
+        if SINGLE:
+            w(f"    float cs[{sp}], xs[{nr}];")
+        w(f"    float xd[{nd}];")
         w("#pragma unroll")
-        w("    for (int k = 0; k < SMAX; ++k) c[k] = 0.f;")
+        w(f"    for (int k = 0; k < {sp}; ++k) {{")
+        for i in range(NPAIR):
+            w(f"        cp{i}[k] = f2{{0.f, 0.f}};")
+        if SINGLE:
+            w("        cs[k] = 0.f;")
+        w("    }")
+        w("    // this thread's channel values, loaded once for all T iterations")
+        for n, j in enumerate(S.reg_cols[p]):
+            for i in range(NPAIR):
+                w(f"    xp{i}[{n}] = f2{{bload(xr, vo, {X(j, 2 * i)}), bload(xr, vo, {X(j, 2 * i + 1)})}};")
+            if SINGLE:
+                w(f"    xs[{n}] = bload(xr, vo, {X(j, Q - 1)});")
+        for n, j in enumerate(S.d1_cols[p]):
+            for q in range(Q):
+                w(f"    xd[{n * Q + q}] = bload(xr, vo, {X(j, q)});")
         w("    for (int it = 0; it < a.T; ++it) {")
         w("        const float* pp = it >= 1 ? a.outs.p[it - 1] : nullptr;  // previous iteration's posterior")
         w(f"        const rsrc_t pr = make_rsrc(pp ? pp + blk * {NZ} : a.xa, pp ? nlive * {4 * NZ} : 0);  // no output: stores dropped")
         if "vn" not in SKIP:
-            w(f"        vn_p{p}<KIND>(c, a, xr, vo, it, pr);")
+            w(f"        vn_p{p}<KIND>({state_args()}, {x_args()}, a, vo, it, pr);")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
         w(f"        const rsrc_t nr = make_rsrc(pn ? pn + blk * {NZ} : a.xa, pn ? nlive * {4 * NZ} : 0);")
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
         for ci in range(len(S.chunks)):
-            w(f"        wr_p{p}_c{ci}<KIND>(c, lds, u, a, xr, vo, it);")
+            w(f"        wr_p{p}_c{ci}<KIND>({state_args()}, {x_args()}, lds, u, a, it);")
             w("        __syncthreads();")
             if "cn" not in SKIP:
                 for dc, t0, n in S.cn_groups[(p, ci)]:
                     w(f"        cn_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]});")
             w("        __syncthreads();")
-            w(f"        rd_p{p}_c{ci}<KIND>(c, lds, u, a, xr, vo, nr, cr, vc, co_last);")
+            w(f"        rd_p{p}_c{ci}<KIND>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last);")
             w("        __syncthreads();")
         w("    }")
         w("    const float* pl = a.outs.p[a.T - 1];")
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
-        w(f"    post_p{p}<KIND>(c, a, xr, vo, a.T, lr);")
+        w(f"    post_p{p}<KIND>({state_args()}, {x_args()}, a, vo, a.T, lr);")
         w("    if (a.c2v_out) {")
         for q in range(Q):
             for k, e in enumerate(S.slots[p]):
-                w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, c[{sl(p, q, k)}]);")
+                w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, {ref(q, k)});")
         w("    }")
         w("}")
     w("template <int KIND>")

@@ -51,6 +51,22 @@ __device__ __forceinline__ float posterior(float xav, float P, const FusedArgs& 
     return clampf(fadd(xo, P), a.lo, a.hi);
 }
 
+// Two variable copies at once.  f2 arithmetic is per-lane IEEE fp32 (v_pk_add_f32 on gfx950: two
+// correctly rounded adds), so a pair computes exactly what two scalar copies would.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int KIND>
+__device__ __forceinline__ f2 posterior2(f2 xav, f2 P, const FusedArgs& a) {
+    if (KIND == NLDPC_NEURAL) return xav + P;
+    return f2{posterior<KIND>(xav.x, P.x, a), posterior<KIND>(xav.y, P.y, a)};
+}
+
+template <int KIND>
+__device__ __forceinline__ f2 vn_channel2(f2 xa, const float* w_vn, int N, int j, int steps, int qbit) {
+    if (KIND == NLDPC_NEURAL) return xa;
+    return f2{vn_channel<KIND>(xa.x, w_vn, N, j, steps, qbit), vn_channel<KIND>(xa.y, w_vn, N, j, steps, qbit)};
+}
+
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
 // scalar loads (a row's edges are consecutive in C order: one s_load_dwordx8/x16 per row).
 typedef const float __attribute__((address_space(4)))* cfloat_p;
@@ -58,7 +74,8 @@ typedef const float __attribute__((address_space(4)))* cfloat_p;
 // Neural check node of one check copy of a degree-DC row, in place: m[k] (gathered v2c) -> c2v, with
 // the reference's arithmetic (NeuralLDPCDecoder.py:74-91) specialised to what the Neural rule can
 // produce.  The magnitude is min(10000, min over the OTHER edges' nonzero |m|); with the ordering key
-// bits(|x|) - 1 (unsigned: exact zeros become the largest key, positive floats keep their order) the
+// (bits(x) << 1) - 2 = 2*bits(|x|) - 2 (unsigned: exact zeros of either sign wrap to the largest keys,
+// nonzero magnitudes keep their order, NaNs sort above 10000 and never win, as in cn_core) the
 // two smallest keys are tracked branch-free, and an edge whose key equals the minimum gets the second
 // minimum (ties give min1 == min2, as the first-index argmin of cn_core does).  sign: +1 iff the
 // number of strictly positive OTHER inputs is odd (x_output_0's sign product).  The epilogue is
@@ -66,24 +83,25 @@ typedef const float __attribute__((address_space(4)))* cfloat_p;
 // (tests compare the fused and streaming paths).
 template <int DC>
 __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
-    constexpr uint32_t kInit = 0x461C3FFFu;  // bits(10000.f) - 1
+    constexpr uint32_t kInit = (0x461C4000u << 1) - 2u;  // key of 10000.f
     uint32_t min1 = kInit, min2 = kInit;
     uint32_t key[DC];
     bool pos[DC];
     bool par = false;
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        key[k] = (__builtin_bit_cast(uint32_t, m[k]) & 0x7fffffffu) - 1u;
+        key[k] = (__builtin_bit_cast(uint32_t, m[k]) << 1) - 2u;  // one v_lshl_add_u32
         pos[k] = m[k] > 0.f;
         par ^= pos[k];
         min2 = min(min2, max(min1, key[k]));
         min1 = min(min1, key[k]);
     }
-    const float f1 = __builtin_bit_cast(float, min1 + 1u);
-    const float f2 = __builtin_bit_cast(float, min2 + 1u);
+    float mg1 = __builtin_bit_cast(float, (min1 + 2u) >> 1);
+    float mg2 = __builtin_bit_cast(float, (min2 + 2u) >> 1);
+    asm volatile("" : "+v"(mg1), "+v"(mg2));  // decode once per row, not after every per-edge select
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        const float mag = key[k] == min1 ? f2 : f1;
+        const float mag = key[k] == min1 ? mg2 : mg1;
         const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
         m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
     }

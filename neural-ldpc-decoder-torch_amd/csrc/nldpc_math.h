@@ -44,18 +44,18 @@ __device__ __forceinline__ QRange q_range(int q) {
 }
 
 __device__ __forceinline__ float quantize(float x, int q) {
-    float qv;
-    switch (q) {
-        case 6: qv = clampf(rintf(x), -15.5f, 15.5f); break;
-        case 5: qv = clampf(fmul(rintf(fmul(x, 2.f)), 0.5f), -7.5f, 7.5f); break;
-        case -5: qv = clampf(rintf(x), -15.f, 15.f); break;
-        case 4: qv = clampf(rintf(x), -7.f, 7.f); break;
-        case 3: qv = clampf(fmul(rintf(fmul(x, 0.5f)), 2.f), -6.f, 6.f); break;
-        default: return x;
-    }
-    const QRange r = q_range(q);
-    const float xc = clampf(x, r.lo, r.hi);
-    return fadd(xc, __fsub_rn(qv, xc));
+    // Branch-free over the (wave-uniform) q: every active q is clamp(rint(x*s)/s) with s in {2, 1, 1/2},
+    // where the scalings are exact, so this equals the per-q formulas of the reference bit for bit:
+    // q=5 rint(2x)/2 in +-7.5, q=6 rint(x) in +-15.5, q=-5 rint(x) in +-15, q=4 rint(x) in +-7,
+    // q=3 rint(x/2)*2 in +-6.  The parameter selects are scalar and hoisted out of loops.
+    const float s = q == 5 ? 2.f : (q == 3 ? 0.5f : 1.f);
+    const float inv = q == 5 ? 0.5f : (q == 3 ? 2.f : 1.f);
+    const float hi = q == 6 ? 15.5f : (q == 5 ? 7.5f : (q == -5 ? 15.f : (q == 4 ? 7.f : 6.f)));
+    const bool active = q == 6 || q == 5 || q == -5 || q == 4 || q == 3;
+    const float qv = clampf(fmul(rintf(fmul(x, s)), inv), -hi, hi);
+    const float xc = clampf(x, -hi, hi);
+    const float r = fadd(xc, __fsub_rn(qv, xc));
+    return active ? r : x;
 }
 
 // STE / clamp gradient mask: 1 on the closed interval (torch.clamp backward), else 0
