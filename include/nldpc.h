@@ -147,10 +147,11 @@ int nldpc_ber_count(const float* llr, const uint8_t* y, int64_t B, int64_t L, in
 int nldpc_awgn_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,
                    int32_t qbit, void* stream);
 
-/* ---- benchmark instrumentation: per-kernel HIP-event timing of nldpc_forward launches.
- *   nldpc_profile_begin arms a recorder for up to `capacity` launches (not thread-safe);
+/* ---- benchmark instrumentation: per-kernel HIP-event timing of nldpc_forward / nldpc_backward
+ *   launches.  nldpc_profile_begin arms a recorder for up to `capacity` launches (not thread-safe);
  *   nldpc_profile_end synchronises on the recorded events and returns summed milliseconds and
- *   launch counts per kernel kind (0 = variable-node, 1 = check-node, 2 = final posterior). */
+ *   launch counts per kernel kind (0 = variable-node, 1 = check-node, 2 = final posterior,
+ *   3 = fused decoder, 4 = variable-node backward, 5 = check-node backward). */
 int nldpc_profile_begin(int32_t capacity);
 int nldpc_profile_end(int32_t nkinds, float* ms, int32_t* count);
 

@@ -292,7 +292,9 @@ template <int DV, int KIND>
 static hipError_t launch_vnb(const VNBArgs& a, hipStream_t s) {
     dim3 grid, block;
     node_geometry(a.B, a.g.Z, a.g.N, grid, block);
+    prof_start(PROF_VNB, s);
     hipLaunchKernelGGL((vnb_kernel<DV, KIND>), grid, block, 0, s, a);
+    prof_stop(s);
     return hipGetLastError();
 }
 
@@ -319,7 +321,9 @@ template <int DC, int KIND, bool UCN>
 static hipError_t launch_cnb(const CNBArgs& a, hipStream_t s) {
     dim3 grid, block;
     node_geometry(a.B, a.g.Z, a.g.M, grid, block);
+    prof_start(PROF_CNB, s);
     hipLaunchKernelGGL((cnb_kernel<DC, KIND, UCN>), grid, block, 0, s, a);
+    prof_stop(s);
     return hipGetLastError();
 }
 

@@ -69,7 +69,7 @@ SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
 int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T);
 
 // benchmark instrumentation (nldpc_profile.cpp)
-enum ProfKind { PROF_VN = 0, PROF_CN = 1, PROF_POST = 2, PROF_FUSED = 3 };
+enum ProfKind { PROF_VN = 0, PROF_CN = 1, PROF_POST = 2, PROF_FUSED = 3, PROF_VNB = 4, PROF_CNB = 5 };
 bool prof_armed();
 void prof_start(int kind, hipStream_t s);
 void prof_stop(hipStream_t s);

@@ -131,3 +131,30 @@ def test_oracle_quantizer(golden):
     x = torch.from_numpy(d["x"])
     for qb, key in ((6, "q6"), (5, "q5"), (-5, "q5m"), (4, "q4"), (3, "q3"), (7, "q7")):
         assert np.array_equal(quantize(x, qb).numpy(), d[key]), key
+
+
+def test_oracle_reproduces_reference_ber_curve(golden):
+    """The oracle's per-iteration error counts equal the reference decoder's over the whole z=16 BER
+    curve (tests/golden/gen_ber_curve.py: 250 codewords per Eb/N0 point, 1.0..4.0 dB, T=20)."""
+    import hashlib
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "neural-ldpc-decoder-torch_amd", "src"))
+    import neural_ldpc_decoder as nd
+    d = golden("ber_curve_neural_bg2_z16")
+    bg = np.loadtxt(os.path.join(ROOT, "resources", "basegraph2_set0.txt"), int, delimiter="\t")
+    gen16 = np.loadtxt(os.path.join(ROOT, "resources", "gen_matrix_bg2_z16.txt"), int, delimiter=",")
+    M, N = bg.shape
+    W, T, Z = int(d["words"]), int(d["T"]), int(d["Z"])
+    xs, ys = nd.AWGNPassedDatagen(N=N, M=M, snr_db=d["ebn0_db"].copy(), gen_matrix=gen16)(
+        word_length=W, Z=Z, is_y_all_zero=True)
+    g = OracleGraph(bg, Z)
+    w = [torch.full((g.E,), 0.5) for _ in range(T)]
+    b = [torch.zeros(g.E) for _ in range(T)]
+    for k in range(len(d["ebn0_db"])):
+        x = np.reshape(xs[k], [W, N, Z]).astype(np.float32)
+        assert hashlib.sha256(x.tobytes()).hexdigest() == str(d["x_sha256"][k])
+        y = np.asarray(ys[k]).reshape(W, N * Z)
+        outs = neural_forward(g, torch.from_numpy(x), w, b)
+        wrong = [(o.numpy() > 0) != y for o in outs]
+        assert [int(m.sum()) for m in wrong] == d["bit_errors"][k].tolist()
+        assert [int(m.any(axis=1).sum()) for m in wrong] == d["frame_errors"][k].tolist()
