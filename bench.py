@@ -34,9 +34,9 @@ for p in (os.path.join(ROOT, "neural-ldpc-decoder-torch_amd", "src"), ROOT):
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, Chip-level parameters)
 METRIC = "codewords/sec + BER@Eb/N0, 5G-NR BG2 z=384, 20 iters, 1/2/4/8 MI355X"
-KINDS = ("vn", "cn", "post", "fused", "vnb", "cnb")
+KINDS = ("vn", "cn", "post", "fused", "vnb", "cnb", "fusedb")
 KERNEL_NAMES = {"vn": "vn_kernel", "cn": "cn_kernel", "post": "vn_kernel (final posterior)",
-                "fused": "fused_<graph>::kernel", "vnb": "vnb_kernel", "cnb": "cnb_kernel"}
+                "fused": "fused_<graph>::kernel", "vnb": "vnb_kernel", "cnb": "cnb_kernel", "fusedb": "fusedb_<graph>::bwd_kernel"}
 WORKLOADS = {
     # name: (base graph file, Z, T, default per-GPU batch)
     "cfg3": ("basegraph2_set0.txt", 384, 20, 65536),
@@ -79,7 +79,8 @@ def kernel_bytes(B, E, N, Z, T):
     vnb = B * f * (E * Z + N * Z)                 # per iteration: grad of the posterior in, grad v2c out
     cnb = B * f * (2 * E * Z)                     # per iteration: saved v2c + grad c2v in
     return {"vn": vn_first + (T - 1) * vn, "cn": T * cn, "post": post, "fused": fused,
-            "fused_compulsory": B * f * (T + 1) * N * Z, "vnb": (T + 1) * vnb, "cnb": T * cnb}
+            "fused_compulsory": B * f * (T + 1) * N * Z, "vnb": (T + 1) * vnb, "cnb": T * cnb,
+            "fusedb": B * f * T * (3 * E * Z + N * Z)}
 
 
 class Prof:

@@ -1,4 +1,4 @@
-"""Generate the register-resident fused decoder kernels (nldpc_fused_gen.hip) for known base graphs.
+"""Generate the register-resident fused decoder kernels (lib/gen/fused_*.hip) for known base graphs.
 
 Design (DESIGN.md §Fused kernel): one workgroup decodes G codewords for all T iterations without
 touching HBM for message state.  The c2v messages of a codeword (E*Z floats, 302 KB for BG2 z=384)
@@ -17,7 +17,7 @@ Everything that indexes registers is emitted as straight-line code with literal 
 generator needs the graph structure at build time; the per-edge arithmetic is the shared
 nldpc_node.h / nldpc_fused.h code, identical to the streaming kernels (tests compare both paths).
 
-Usage: python3 gen_fused.py OUT.hip RESOURCE_DIR
+Usage: python3 gen_fused.py OUTDIR RESOURCE_DIR   (or --list: the generated file names)
 """
 import os
 import sys
@@ -157,8 +157,7 @@ def emit(S: Spec) -> str:
         w(f"        {{  // column {j}, degree {d}, {'copies ' + xin if vec else 'copy ' + xin}")
         w(f"            {T_} P = {zero};")
         if not final:
-            ch = (f"vn_channel2<KIND>({xin}, a.w_vn, N, {j}, a.vn_prefix + it + 1, a.qbit)" if vec else
-                  f"vn_channel<KIND>({xin}, a.w_vn, N, {j}, a.vn_prefix + it + 1, a.qbit)")
+            ch = f"chan2<KIND>({xin}, a)" if vec else f"chan<KIND>({xin}, a)"
             w(f"            const {T_} x0 = {add(zero, ch)};")
             for k in range(d):
                 expr = "P"
@@ -178,22 +177,39 @@ def emit(S: Spec) -> str:
         cols = S.reg_cols[p]
         for final in (False, True):
             fname = f"post_p{p}" if final else f"vn_p{p}"
-            w("template <int KIND>")
+            w("template <int KIND, bool SAVE>")
             w(f"__device__ __forceinline__ void {fname}({state_params(p)}, {x_params(p)}, const FusedArgs& a, "
-              f"uint32_t vo, int it, rsrc_t pr) {{")
+              f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm) {{")
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
                 for i in range(NPAIR):
                     vn_group(p, n, j, s, d, final, True, f"cp{i}", f"xp{i}[{n}]")
-                    w(f"            const f2 y_ = posterior2<KIND>(xp{i}[{n}], P, a);")
-                    w(f"            bstore(pr, vo, {X(j, 2 * i)}, y_.x);")
-                    w(f"            bstore(pr, vo, {X(j, 2 * i + 1)}, y_.y);")
+                    w(f"            const f2 xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? f2{{bload(xr, vo, {X(j, 2 * i)}), "
+                      f"bload(xr, vo, {X(j, 2 * i + 1)})}} : xp{i}[{n}];")
+                    w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
+                    w("                bool m0_, m1_;")
+                    w(f"                bstore(pr, vo, {X(j, 2 * i)}, posterior_m<KIND>(xo_.x, P.x, a, m0_));")
+                    w(f"                bstore(pr, vo, {X(j, 2 * i + 1)}, posterior_m<KIND>(xo_.y, P.y, a, m1_));")
+                    w(f"                bstore8(pm, vm, {X(j, 2 * i) // 4}, m0_);")
+                    w(f"                bstore8(pm, vm, {X(j, 2 * i + 1) // 4}, m1_);")
+                    w("            } else {")
+                    w("                const f2 y_ = posterior2<KIND>(xo_, P, a);")
+                    w(f"                bstore(pr, vo, {X(j, 2 * i)}, y_.x);")
+                    w(f"                bstore(pr, vo, {X(j, 2 * i + 1)}, y_.y);")
+                    w("            }")
                     w("        }")
                     w("        __builtin_amdgcn_sched_barrier(0);")
                 if SINGLE:
                     vn_group(p, n, j, s, d, final, False, "cs", f"xs[{n}]")
-                    w(f"            bstore(pr, vo, {X(j, Q - 1)}, posterior<KIND>(xs[{n}], P, a));")
+                    w(f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, Q - 1)}) : xs[{n}];")
+                    w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
+                    w("                bool m_;")
+                    w(f"                bstore(pr, vo, {X(j, Q - 1)}, posterior_m<KIND>(xo_, P, a, m_));")
+                    w(f"                bstore8(pm, vm, {X(j, Q - 1) // 4}, m_);")
+                    w("            } else {")
+                    w(f"                bstore(pr, vo, {X(j, Q - 1)}, posterior<KIND>(xo_, P, a));")
+                    w("            }")
                     w("        }")
                     w("        __builtin_amdgcn_sched_barrier(0);")
                 s += d
@@ -214,28 +230,35 @@ def emit(S: Spec) -> str:
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
             mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
             d1 = [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
-            w("template <int KIND>")
+            w("template <int KIND, bool SAVE>")
             w(f"__device__ __forceinline__ void wr_p{p}_c{ci}({state_params(p, True)}, {x_params(p)}, float* lds, "
-              f"int u, const FusedArgs& a, int it) {{")
+              f"int u, const FusedArgs& a, int it, rsrc_t sv, uint32_t vc) {{")
             w("    asm volatile(\"\" : \"+v\"(u));  // LDS addresses are recomputed here, not hoisted out of the loop")
             for q in range(Q):
                 for k, e in mine:
                     w(f"    lds[{own(e, q, e0)}] = {ref(q, k)};")
+                    w(f"    if constexpr (SAVE) bstore(sv, vc, {4 * (e * Z + q * ZT)}, {ref(q, k)});")
             for j, e in d1:  # v2c = (0 + xin) + 0: no other edge in the column
                 for q in range(Q):
-                    w(f"    lds[{own(e, q, e0)}] = fadd(fadd(0.f, vn_channel<KIND>({xref(p, j, q)}, "
-                      f"a.w_vn, N, {j}, a.vn_prefix + it + 1, a.qbit)), 0.f);")
+                    w(f"    {{ const float v_ = fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f); "
+                      f"lds[{own(e, q, e0)}] = v_; if constexpr (SAVE) bstore(sv, vc, {4 * (e * Z + q * ZT)}, v_); }}")
             w("}")
-            w("template <int KIND>")
+            w("template <int KIND, bool SAVE>")
             w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
-              f"int u, const FusedArgs& a, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co) {{")
+              f"int u, const FusedArgs& a, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co, "
+              f"uint32_t vm, rsrc_t xr, rsrc_t pm) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
             for q in range(Q):
                 for k, e in mine:
                     w(f"    {ref(q, k)} = lds[{own(e, q, e0)}];")
             for j, e in d1:  # this iteration's posterior right away
                 for q in range(Q):
-                    w(f"    bstore(pr, vo, {X(j, q)}, posterior<KIND>({xref(p, j, q)}, fadd(0.f, lds[{own(e, q, e0)}]), a));")
+                    w(f"    {{ const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
+                    w(f"      const float P_ = fadd(0.f, lds[{own(e, q, e0)}]);")
+                    w("      if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
+                    w(f"          bool m_; bstore(pr, vo, {X(j, q)}, posterior_m<KIND>(xo_, P_, a, m_)); "
+                      f"bstore8(pm, vm, {X(j, q) // 4}, m_);")
+                    w(f"      }} else {{ bstore(pr, vo, {X(j, q)}, posterior<KIND>(xo_, P_, a)); }} }}")
             if d1:
                 w("    if (has_co) {  // final message state (last iteration only)")
                 for j, e in d1:
@@ -259,7 +282,7 @@ def emit(S: Spec) -> str:
                 tab += [S.row_edges[i][0] for i in sel]
             groups[(p, ci)] = gl
     S.cn_groups = groups
-    w(f"__constant__ int32_t cn_tab[{max(1, len(tab))}] = {{{', '.join(str(x) for x in tab) or '0'}}};")
+    w(f"static __constant__ int32_t cn_tab[{max(1, len(tab))}] = {{{', '.join(str(x) for x in tab) or '0'}}};")
     w("template <int KIND, int DC>")
     w("__device__ __forceinline__ void cn_rows(float* lds, int u, const FusedArgs& a, int it, int t0, int n, int e0c) {")
     w("    asm volatile(\"\" : \"+v\"(u));")
@@ -321,9 +344,9 @@ def emit(S: Spec) -> str:
             continue
         sp = max(len(S.slots[p]), 1)
         nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
-        w("template <int KIND>")
+        w("template <int KIND, bool SAVE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
-          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc) {{")
+          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm) {{")
         for i in range(NPAIR):
             w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
         if SINGLE:
@@ -345,34 +368,76 @@ def emit(S: Spec) -> str:
         for n, j in enumerate(S.d1_cols[p]):
             for q in range(Q):
                 w(f"    xd[{n * Q + q}] = bload(xr, vo, {X(j, q)});")
+        # cumulative VN weighting: the channel registers hold xin and advance one step per iteration
+        def chan_steps(step_expr, indent):
+            w(f"{indent}{{ const cfloat_p wr_ = (cfloat_p)(a.w_vn + (int64_t)({step_expr}) * N);")
+            for n, j in enumerate(S.reg_cols[p]):
+                for i in range(NPAIR):
+                    for c in "xy":
+                        w(f"{indent}  xp{i}[{n}].{c} = chan_step<KIND>(xp{i}[{n}].{c}, a, wr_[{j}]);")
+                if SINGLE:
+                    w(f"{indent}  xs[{n}] = chan_step<KIND>(xs[{n}], a, wr_[{j}]);")
+            for n, j in enumerate(S.d1_cols[p]):
+                for q in range(Q):
+                    w(f"{indent}  xd[{n * Q + q}] = chan_step<KIND>(xd[{n * Q + q}], a, wr_[{j}]);")
+            w(f"{indent}}}")
+
+        def rs(ptr, size):  # descriptor over this block's part of a per-iteration buffer, or an empty one
+            return f"make_rsrc({ptr} ? {ptr} + blk * {size} : a.xa, {ptr} ? nlive * {size} : 0)"
+
+        w("    if (KIND != NLDPC_NEURAL && a.w_vn) {  // steps applied before this call's first iteration")
+        w("        for (int s_ = 0; s_ < a.vn_prefix; ++s_)")
+        chan_steps("s_", "            ")
+        w("    }")
         w("    for (int it = 0; it < a.T; ++it) {")
+        w("        if (KIND != NLDPC_NEURAL && a.w_vn) {")
+        chan_steps("a.vn_prefix + it", "            ")
+        w("            if constexpr (SAVE) {")
+        w("                float* sx_ = a.sxin ? a.sxin + it * a.sxin_stride : nullptr;")
+        w(f"                const rsrc_t sx = make_rsrc(sx_ ? sx_ + blk * {NZ} : a.xa, sx_ ? nlive * {4 * NZ} : 0);")
+        for n, j in enumerate(S.reg_cols[p]):
+            for q in range(Q):
+                w(f"                bstore(sx, vo, {X(j, q)}, {xref(p, j, q)});")
+        for n, j in enumerate(S.d1_cols[p]):
+            for q in range(Q):
+                w(f"                bstore(sx, vo, {X(j, q)}, {xref(p, j, q)});")
+        w("            }")
+        w("        }")
         w("        const float* pp = it >= 1 ? a.outs.p[it - 1] : nullptr;  // previous iteration's posterior")
         w(f"        const rsrc_t pr = make_rsrc(pp ? pp + blk * {NZ} : a.xa, pp ? nlive * {4 * NZ} : 0);  // no output: stores dropped")
+        w("        const uint8_t* pmp = (SAVE && a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
+        w(f"        const rsrc_t pm = make_rsrc((const float*)(pmp ? pmp + blk * {NZ} : nullptr), pmp ? nlive * {NZ} : 0);")
         if "vn" not in SKIP:
-            w(f"        vn_p{p}<KIND>({state_args()}, {x_args()}, a, vo, it, pr);")
+            w(f"        vn_p{p}<KIND, SAVE>({state_args()}, {x_args()}, a, vo, it, pr, vm, xr, pm);")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
         w(f"        const rsrc_t nr = make_rsrc(pn ? pn + blk * {NZ} : a.xa, pn ? nlive * {4 * NZ} : 0);")
+        w("        const uint8_t* nmp = (SAVE && a.symask) ? a.symask + it * a.symask_stride : nullptr;")
+        w(f"        const rsrc_t nm = make_rsrc((const float*)(nmp ? nmp + blk * {NZ} : nullptr), nmp ? nlive * {NZ} : 0);")
+        w("        float* svp = SAVE ? a.sv2c + it * a.sv2c_stride : nullptr;")
+        w(f"        const rsrc_t sv = make_rsrc(svp ? svp + blk * {S.E * Z} : a.xa, svp ? nlive * {4 * S.E * Z} : 0);")
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
         for ci in range(len(S.chunks)):
-            w(f"        wr_p{p}_c{ci}<KIND>({state_args()}, {x_args()}, lds, u, a, it);")
+            w(f"        wr_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, it, sv, vc);")
             w("        __syncthreads();")
             if "cn" not in SKIP:
                 for dc, t0, n in S.cn_groups[(p, ci)]:
                     w(f"        cn_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]});")
             w("        __syncthreads();")
-            w(f"        rd_p{p}_c{ci}<KIND>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last);")
+            w(f"        rd_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm);")
             w("        __syncthreads();")
         w("    }")
         w("    const float* pl = a.outs.p[a.T - 1];")
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
-        w(f"    post_p{p}<KIND>({state_args()}, {x_args()}, a, vo, a.T, lr);")
+        w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
+        w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
+        w(f"    post_p{p}<KIND, SAVE>({state_args()}, {x_args()}, a, vo, a.T, lr, vm, xr, lm);")
         w("    if (a.c2v_out) {")
         for q in range(Q):
             for k, e in enumerate(S.slots[p]):
                 w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, {ref(q, k)});")
         w("    }")
         w("}")
-    w("template <int KIND>")
+    w("template <int KIND, bool SAVE>")
     w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void kernel(FusedArgs a) {{")
     w(f"    __shared__ float lds_all[{CF * G}];")
     w("    const int t = threadIdx.x;")
@@ -390,54 +455,378 @@ def emit(S: Spec) -> str:
     w(f"    const rsrc_t xr = make_rsrc(a.xa + blk * {NZ}, nlive * {4 * NZ});")
     w(f"    const rsrc_t cr = make_rsrc(a.c2v_out ? a.c2v_out + blk * {S.E * Z} : a.xa, nlive * {4 * S.E * Z});")
     w(f"    float* lds = lds_all + g * {CF};")
-    each_part("run_p{p}<KIND>(a, lds, u, blk, nlive, xr, vo, cr, vc)", indent="    ")
+    w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
+    each_part("run_p{p}<KIND, SAVE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm)", indent="    ")
     w("}")
-    w(f"static const int32_t basegraph[{S.M * S.N}] = {{{', '.join(str(int(x)) for x in S.hb.reshape(-1))}}};")
+    w("}  // namespace")
+    return "\n".join(L)
+
+
+def emit_bwd(S: Spec) -> str:
+    """Backward kernels (training): the forward's ownership and LDS exchange, run in reverse.
+
+    State: dL/dc2v_{k+1} of every register edge copy (the forward's c2v slots), one float array per
+    lane copy.  Per iteration k = T-1..0: owners write the state into the check-ordered LDS image
+    (degree-1 edges: dL/dy_k * mask_k), the check-node threads gather v2c_k from the saved buffer at
+    the cyclic shift, run cn_backward (nldpc_node.h, the streaming cnb_kernel's arithmetic) and put
+    dL/dv2c_k back in place, owners read it back; then the variable-node step: dL/dc2v_k = dL/dy_{k-1}
+    * mask_{k-1} + sum of the column's other dL/dv2c_k (prefix + suffix, as vnb_kernel), and the
+    cumulative VN-weight chain (carry per channel value).  Weight gradients: per-wave partial sums."""
+    Z, G, Q, ZT, NZ, E, N = S.Z, S.G, S.Q, S.ZT, S.N * S.Z, S.E, S.N
+    WP = S.lanes // 64  # waves per part
+    L = []
+    w = L.append
+    CF = S.chunk_floats
+    w(f"// ---- {S.tag} backward: {S.threads} threads, {WP} wave(s) per part")
+    w(f"namespace fusedb_{S.tag} {{")
+    w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {N}, E = {E}, WP = {WP};")
+
+    def X(j, q):
+        return 4 * (j * Z + q * ZT)
+
+    def own(e, q, e0):
+        cq = (q * ZT - int(S.shift[e])) % Z
+        base = (e - e0) * Z + cq
+        if cq + ZT <= Z:
+            return f"{base} + u"
+        return f"{base} + u - (u >= {Z - cq} ? {Z} : 0)"
+
+    def sref(q, k):
+        return f"g{q}[{k}]"
+
+    def state_params(p):
+        sp = max(len(S.slots[p]), 1)
+        return ", ".join(f"float (&g{q})[{sp}]" for q in range(Q))
+
+    def state_args():
+        return ", ".join(f"g{q}" for q in range(Q))
+
+    # the VN-weight chain of one channel value: carry (a workspace buffer, one float per variable copy:
+    # registers are all taken by the state) and this column's weight-gradient contribution
+    # (vnb_kernel's arithmetic: u = xprev * w, STE mask of Q on u, du = (gsum + carry) * mask)
+    def chain(p, j, q, gsum, indent):
+        w(f"{indent}{{ const float xp_ = it >= 1 ? bload(sxp, vo, {X(j, q)}) : bload(xr, vo, {X(j, q)});")
+        w(f"{indent}  const float u_ = fmul(xp_, wvn[{j}]);")
+        w(f"{indent}  const float mk_ = (KIND == NLDPC_QMS && qr.active) ? in_range(u_, qr.lo, qr.hi) : 1.f;")
+        w(f"{indent}  const float cy_ = it == a.T - 1 ? 0.f : bload(cyr, vo, {X(j, q)});")
+        w(f"{indent}  const float du_ = ({gsum} + cy_) * mk_;")
+        w(f"{indent}  ctb_ += du_ * xp_;")
+        w(f"{indent}  bstore(cyr, vo, {X(j, q)}, du_ * wvn[{j}]); }}")
+
+    def col_partial(j, indent):
+        w(f"{indent}if (a.p_vn) {{ const float s_ = wave_sum(ctb_); if (lane0) a.p_vn[pv + {j}] = s_; }}")
+
+    # ---------------------------------------------------------------- LDS write / read-back
+    for p in range(S.P):
+        for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
+            mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
+            d1 = [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
+            w("template <int KIND>")
+            w(f"__device__ __forceinline__ void wrb_p{p}_c{ci}({state_params(p)}, float* lds, int u, rsrc_t gr, "
+              f"rsrc_t mr, uint32_t vo, uint32_t vm) {{")
+            w("    asm volatile(\"\" : \"+v\"(u));")
+            for q in range(Q):
+                for k, e in mine:
+                    w(f"    lds[{own(e, q, e0)}] = {sref(q, k)};")
+            for j, e in d1:  # dL/dc2v_{k+1} of a degree-1 edge: only its own posterior
+                for q in range(Q):
+                    w(f"    lds[{own(e, q, e0)}] = gy_masked<KIND>(gr, mr, vo, vm, {X(j, q)});")
+            w("}")
+            w("template <int KIND>")
+            w(f"__device__ __forceinline__ void rdb_p{p}_c{ci}({state_params(p)}, const float* lds, "
+              f"int u, const FusedBwdArgs& a, int it, uint32_t vo, rsrc_t xr, rsrc_t sxp, rsrc_t cyr, cfloat_p wvn, "
+              f"int64_t pv, bool lane0) {{")
+            w("    asm volatile(\"\" : \"+v\"(u));")
+            for q in range(Q):
+                for k, e in mine:
+                    w(f"    {sref(q, k)} = lds[{own(e, q, e0)}];")
+            if d1:
+                w("    if (KIND != NLDPC_NEURAL && a.w_vn) {  // VN chain of the degree-1 columns (gsum = their one edge)")
+                w("        const QRange qr = q_range(a.qbit);")
+                for j, e in d1:
+                    w("        { float ctb_ = 0.f;")
+                    for q in range(Q):
+                        w(f"          {{ const float gs_ = 0.f + lds[{own(e, q, e0)}];")
+                        chain(p, j, q, "gs_", "            ")
+                        w("          }")
+                        w("          __builtin_amdgcn_sched_barrier(0);")
+                    col_partial(j, "          ")
+                    w("        }")
+                w("    }")
+            w("}")
+
+    # ---------------------------------------------------------------- variable-node backward
+    for p in range(S.P):
+        w("template <int KIND>")
+        w(f"__device__ __forceinline__ void vnb_p{p}({state_params(p)}, const FusedBwdArgs& a, "
+          f"int it, uint32_t vo, uint32_t vm, rsrc_t gr, rsrc_t mr, rsrc_t xr, rsrc_t sxp, rsrc_t cyr, cfloat_p wvn, "
+          f"int64_t pv, bool lane0) {{")
+        w("    const bool chain_on = KIND != NLDPC_NEURAL && a.w_vn;")
+        w("    const QRange qr = q_range(a.qbit);")
+        s0 = 0
+        for j in S.reg_cols[p]:
+            d = len(S.col_edges[j])
+            w(f"    {{  // column {j}, degree {d}")
+            w("        float ctb_ = 0.f;")
+            for q in range(Q):
+                c = lambda k: sref(q, s0 + k)  # noqa: E731
+                w("        {")
+                w("            float gs_ = 0.f;")
+                for k in range(d):
+                    w(f"            gs_ = gs_ + {c(k)};")
+                w("            if (it >= 1) {")
+                w(f"                const float gyv_ = gy_masked<KIND>(gr, mr, vo, vm, {X(j, q)});")
+                w(f"                float suf_[{d + 1}];")
+                w(f"                suf_[{d}] = 0.f;")
+                for k in range(d - 1, -1, -1):
+                    w(f"                suf_[{k}] = suf_[{k + 1}] + {c(k)};")
+                w("                float pre_ = 0.f;")
+                for k in range(d):
+                    w(f"                {{ const float o_ = {c(k)}; {c(k)} = gyv_ + (pre_ + suf_[{k + 1}]); pre_ += o_; }}")
+                w("            }")
+                w("            if (chain_on) {")
+                chain(p, j, q, "gs_", "                ")
+                w("            }")
+                w("        }")
+                w("        __builtin_amdgcn_sched_barrier(0);  // one column copy at a time (register pressure)")
+            w("        if (chain_on) {")
+            col_partial(j, "            ")
+            w("        }")
+            w("    }")
+            s0 += d
+        w("}")
+
+    # ---------------------------------------------------------------- check-node backward (table driven)
+    tab, shifts, groups = [], [], {}
+    for p in range(S.P):
+        for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
+            gl = []
+            rows = S.cn_rows[ci][p]
+            for dc in sorted({len(S.row_edges[i]) for i in rows}, reverse=True):
+                sel = [i for i in rows if len(S.row_edges[i]) == dc]
+                gl.append((dc, len(tab), len(sel)))
+                tab += [S.row_edges[i][0] for i in sel]
+            groups[(p, ci)] = gl
+    w(f"static __constant__ int32_t cn_tab[{max(1, len(tab))}] = {{{', '.join(str(x) for x in tab) or '0'}}};")
+    w(f"static __constant__ int32_t e_shift[{E}] = {{{', '.join(str(int(x)) for x in S.shift)}}};")
+    w("template <int KIND, int DC>")
+    w("__device__ __forceinline__ void cnb_rows(float* lds, int u, const FusedBwdArgs& a, int it, int t0, int n, "
+      "int e0c, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0) {")
+    w("    asm volatile(\"\" : \"+v\"(u));")
+    w("    for (int r = 0; r < n; ++r) {")
+    w("        const int e0 = cn_tab[t0 + r];")
+    w("        float* rp = lds + (e0 - e0c) * Z + u;")
+    w("        float wv[DC], bv[DC];")
+    w("        int sh[DC];")
+    w("        const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + e0) : nullptr;")
+    w("        const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + e0) : nullptr;")
+    w("        if (KIND == NLDPC_NEURAL || wc) {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) wv[k] = wc[k];")
+    w("        } else {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) wv[k] = 1.f;")
+    w("        }")
+    w("        if (KIND == NLDPC_NEURAL) {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) bv[k] = bs[k];")
+    w("        } else {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) bv[k] = 0.f;")
+    w("        }")
+    w("#pragma unroll")
+    w("        for (int k = 0; k < DC; ++k) sh[k] = e_shift[e0 + k];")
+    w("        float gwa[DC], gba[DC];")
+    w("#pragma unroll")
+    w("        for (int k = 0; k < DC; ++k) gwa[k] = gba[k] = 0.f;")
+    w("#pragma unroll")
+    w(f"        for (int q = 0; q < {Q}; ++q) {{")
+    w("            auto load_m = [&](int k) {  // saved v2c of edge k at variable copy (h + s) mod Z, h = u + q*ZT")
+    w("                int t = u + q * ZT + sh[k];")
+    w("                t -= t >= Z ? Z : 0;")
+    w("                return bload(svr, vcw + 4u * (uint32_t)t, 4 * (e0 + k) * Z);")
+    w("            };")
+    w("            if constexpr (KIND == NLDPC_SP) {")
+    w("                float m[DC], gc[DC], gm[DC], gw[DC], gu[DC], gb[DC];")
+    w("#pragma unroll")
+    w("                for (int k = 0; k < DC; ++k) {")
+    w("                    m[k] = load_m(k);")
+    w("                    gc[k] = rp[k * Z + q * ZT];")
+    w("                }")
+    w("                cn_backward<DC, KIND, false>(m, gc, DC, 0.f, wv, wv, bv, wc != nullptr, false, a.qbit, a.lo, a.hi, "
+      "gm, gw, gu, gb);")
+    w("#pragma unroll")
+    w("                for (int k = 0; k < DC; ++k) {")
+    w("                    rp[k * Z + q * ZT] = gm[k];")
+    w("                    gwa[k] += gw[k];")
+    w("                }")
+    w("            } else {")
+    w("                cn_bwd_ms<DC, KIND>(load_m, rp + q * ZT, Z, wv, bv, KIND == NLDPC_NEURAL || wc, a.qbit, a.lo, a.hi, "
+      "gwa, gba);")
+    w("            }")
+    w("            __builtin_amdgcn_sched_barrier(0);  // one check copy at a time: the state owns the registers")
+    w("        }")
+    w("        if (a.p_cn) {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) { const float s_ = wave_sum(gwa[k]); if (lane0) a.p_cn[pc + e0 + k] = s_; }")
+    w("        }")
+    w("        if (KIND == NLDPC_NEURAL && a.p_bias) {")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) { const float s_ = wave_sum(gba[k]); if (lane0) a.p_bias[pc + e0 + k] = s_; }")
+    w("        }")
+    w("    }")
+    w("}")
+
+    # ---------------------------------------------------------------- per-part driver
+    for p in range(S.P):
+        sp = max(len(S.slots[p]), 1)
+        w("template <int KIND>")
+        w(f"__device__ __forceinline__ void bwd_p{p}(const FusedBwdArgs& a, float* lds, int u, int64_t blk, int nlive, "
+          f"uint32_t vo, uint32_t vm, uint32_t vcw, int slot, bool lane0) {{")
+        for q in range(Q):
+            w(f"    float g{q}[{sp}];")
+        w(f"    const rsrc_t cyr = make_rsrc(a.carry ? a.carry + blk * {NZ} : nullptr, a.carry ? nlive * {4 * NZ} : 0);")
+        w(f"    const rsrc_t xr = make_rsrc(a.xa + blk * {NZ}, nlive * {4 * NZ});")
+
+        def rs(ptr_expr, esize, per_cw):
+            return (f"make_rsrc((const float*)({ptr_expr} ? {ptr_expr} + blk * {per_cw} : nullptr), "
+                    f"{ptr_expr} ? nlive * {per_cw * esize} : 0)")
+        w("    {  // k = T-1: dL/dc2v_T = dL/dy_{T-1} * mask (no later check node)")
+        w("        const float* gp_ = a.gy.p[a.T - 1];")
+        w("        const uint8_t* mp_ = a.symask ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
+        w(f"        const rsrc_t gr = {rs('gp_', 4, NZ)};")
+        w(f"        const rsrc_t mr = {rs('mp_', 1, NZ)};")
+        s0 = 0
+        for j in S.reg_cols[p]:
+            d = len(S.col_edges[j])
+            for q in range(Q):
+                w(f"        {{ const float v_ = gy_masked<KIND>(gr, mr, vo, vm, {X(j, q)});")
+                for k in range(d):
+                    w(f"          g{q}[{s0 + k}] = v_;")
+                w("        }")
+            s0 += d
+        w("    }")
+        w("    for (int it = a.T - 1; it >= 0; --it) {")
+        w("        const float* gp_ = a.gy.p[it];")
+        w("        const uint8_t* mp_ = a.symask ? a.symask + it * a.symask_stride : nullptr;")
+        w(f"        const rsrc_t gr = {rs('gp_', 4, NZ)};")
+        w(f"        const rsrc_t mr = {rs('mp_', 1, NZ)};")
+        w("        const float* sv_ = a.sv2c + it * a.sv2c_stride;")
+        w(f"        const rsrc_t svr = make_rsrc(sv_ + blk * {E * Z}, nlive * {4 * E * Z});")
+        w("        const float* sx_ = (a.sxin && it >= 1) ? a.sxin + (it - 1) * a.sxin_stride : nullptr;")
+        w(f"        const rsrc_t sxp = {rs('sx_', 4, NZ)};")
+        w("        const cfloat_p wvn = a.w_vn ? (cfloat_p)(a.w_vn + (int64_t)it * N) : nullptr;")
+        w("        const int64_t pc = ((int64_t)it * a.nslots + slot) * E;")
+        w("        const int64_t pv = ((int64_t)it * a.nslots + slot) * N;")
+        for ci in range(len(S.chunks)):
+            w(f"        wrb_p{p}_c{ci}<KIND>({state_args()}, lds, u, gr, mr, vo, vm);")
+            w("        __syncthreads();")
+            for dc, t0, n in groups[(p, ci)]:
+                w(f"        cnb_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]}, svr, vcw, pc, lane0);")
+            w("        __syncthreads();")
+            w(f"        rdb_p{p}_c{ci}<KIND>({state_args()}, lds, u, a, it, vo, xr, sxp, cyr, wvn, pv, lane0);")
+            w("        __syncthreads();")
+        w("        const float* gq_ = it >= 1 ? a.gy.p[it - 1] : nullptr;  // dL/dy_{k-1}")
+        w("        const uint8_t* mq_ = (a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
+        w(f"        const rsrc_t gr1 = {rs('gq_', 4, NZ)};")
+        w(f"        const rsrc_t mr1 = {rs('mq_', 1, NZ)};")
+        w(f"        vnb_p{p}<KIND>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0);")
+        w("    }")
+        w("}")
+
+    w("template <int KIND>")
+    w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void bwd_kernel(FusedBwdArgs a) {{")
+    w(f"    __shared__ float lds_all[{CF * G}];")
+    w("    const int t = threadIdx.x;")
+    w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes});")
+    w(f"    const int r = t - p * {S.lanes};")
+    w(f"    const int g = r / {ZT};")
+    w(f"    const int u = r - g * {ZT};")
+    w(f"    const int64_t blk = (int64_t)blockIdx.x * {G};")
+    w(f"    const int nlive = a.B - blk < {G} ? (int)(a.B - blk) : {G};")
+    w(f"    const uint32_t vo = g < nlive ? 4u * (g * {NZ} + u) : 0x80000000u;")
+    w("    const uint32_t vm = vo >> 2;")
+    w(f"    const uint32_t vcw = g < nlive ? 4u * (g * {E * Z}) : 0x80000000u;  // codeword base in [E][Z] (CN gathers)")
+    w("    const int slot = blockIdx.x * WP + __builtin_amdgcn_readfirstlane(r >> 6);")
+    w("    const bool lane0 = (t & 63) == 0;")
+    w(f"    float* lds = lds_all + g * {CF};")
+    for p in range(S.P):
+        w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0);")
+    w("}")
     w("}  // namespace")
     return "\n".join(L)
 
 
 def main():
-    out, res = sys.argv[1], sys.argv[2]
+    """Writes OUTDIR/fused_<tag>_s<SAVE>.hip (one translation unit per base graph and SAVE variant,
+    so make -j compiles them in parallel) and OUTDIR/fused_table.hip (the FusedSpec table)."""
+    if sys.argv[1] == "--list":  # file names, for the Makefile
+        print(" ".join([f"fused_{t[0]}_s{v}.hip" for t in SPECS for v in (0, 1)] +
+                       [f"fused_{t[0]}_bwd.hip" for t in SPECS] + ["fused_table.hip"]))
+        return
+    outdir, res = sys.argv[1], sys.argv[2]
+    os.makedirs(outdir, exist_ok=True)
     specs = []
     only = set(filter(None, os.environ.get("NLDPC_GEN_ONLY", "").split(",")))  # debug: subset of specs
     for tag, fname, Z, G, P, Q in SPECS:
-        if only and tag not in only:
-            continue
         hb = np.loadtxt(os.path.join(res, fname), int, delimiter="\t")
-        specs.append(Spec(tag, hb, Z, G, P, Q))
-    src = [
-        "// GENERATED by gen_fused.py from the base graphs in resources/ -- do not edit.",
-        "#include <hip/hip_runtime.h>",
-        '#include "nldpc_fused.h"',
-        "namespace nldpc {",
-    ]
-    for s in specs:
-        src.append(emit(s))
-    src.append("template <int KIND> static void* pick(int i) {")
+        specs.append((Spec(tag, hb, Z, G, P, Q), not only or tag in only))
+    head = ["// GENERATED by gen_fused.py from the base graphs in resources/ -- do not edit.",
+            "#include <hip/hip_runtime.h>", '#include "nldpc_fused.h"', "namespace nldpc {"]
     kinds = os.environ.get("NLDPC_GEN_KINDS")  # debug: instantiate a subset of kinds
-    if kinds:
-        src.append(f"    if constexpr ({' && '.join(f'KIND != {k}' for k in kinds.split(','))}) return nullptr; else {{")
-    for i, s in enumerate(specs):
-        src.append(f"    if (i == {i}) return reinterpret_cast<void*>(&fused_{s.tag}::kernel<KIND>);")
-    src.append("    return nullptr;")
-    if kinds:
-        src.append("    }")
-    src.append("}")
+    kinds = [int(k) for k in kinds.split(",")] if kinds else [0, 1, 2, 3]
+
+    def write(name, lines):
+        path = os.path.join(outdir, name)
+        text = "\n".join(lines) + "\n"
+        if not os.path.exists(path) or open(path).read() != text:  # keep mtimes of unchanged units
+            with open(path, "w") as f:
+                f.write(text)
+
+    for S, on in specs:
+        body = emit(S) if on else ""
+        for save in (0, 1):
+            src = list(head)
+            src.append(body)
+            src.append(f"void* fused_{S.tag}_kernel_s{save}(int kind) {{")
+            if on:
+                for k in kinds:
+                    src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, {'true' if save else 'false'}>);")
+            src.append("    return nullptr;")
+            src.append("}")
+            src.append("}  // namespace nldpc")
+            write(f"fused_{S.tag}_s{save}.hip", src)
+        src = list(head)
+        src.append(emit_bwd(S) if on else "")
+        src.append(f"void* fused_{S.tag}_bwd(int kind) {{")
+        if on:
+            for k in kinds:
+                src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fusedb_{S.tag}::bwd_kernel<{k}>);")
+        src.append("    return nullptr;")
+        src.append("}")
+        src.append("}  // namespace nldpc")
+        write(f"fused_{S.tag}_bwd.hip", src)
+    src = list(head)
+    for S, _ in specs:
+        src.append(f"void* fused_{S.tag}_kernel_s0(int kind);")
+        src.append(f"void* fused_{S.tag}_kernel_s1(int kind);")
+        src.append(f"void* fused_{S.tag}_bwd(int kind);")
+        src.append(f"static const int32_t basegraph_{S.tag}[{S.M * S.N}] = "
+                   f"{{{', '.join(str(int(x)) for x in S.hb.reshape(-1))}}};")
     src.append("const FusedSpec* fused_specs(int* n) {")
     src.append(f"    static const FusedSpec tab[{len(specs)}] = {{")
-    for i, s in enumerate(specs):
-        src.append(f"        {{\"{s.tag}\", {s.M}, {s.N}, {s.Z}, {s.E}, {s.G}, {s.threads}, "
-                   f"fused_{s.tag}::basegraph, {{pick<NLDPC_SP>({i}), pick<NLDPC_MS>({i}), pick<NLDPC_QMS>({i}), "
-                   f"pick<NLDPC_NEURAL>({i})}}}},")
+    for S, _ in specs:
+        k0 = ", ".join(f"fused_{S.tag}_kernel_s0({k})" for k in range(4))
+        k1 = ", ".join(f"fused_{S.tag}_kernel_s1({k})" for k in range(4))
+        kb = ", ".join(f"fused_{S.tag}_bwd({k})" for k in range(4))
+        src.append(f"        {{\"{S.tag}\", {S.M}, {S.N}, {S.Z}, {S.E}, {S.G}, {S.threads}, basegraph_{S.tag}, "
+                   f"{{{{{k0}}}, {{{k1}}}}}, {{{kb}}}, {S.lanes // 64}}},")
     src.append("    };")
     src.append(f"    *n = {len(specs)};")
     src.append("    return tab;")
     src.append("}")
     src.append("}  // namespace nldpc")
-    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
-    with open(out, "w") as f:
-        f.write("\n".join(src) + "\n")
+    write("fused_table.hip", src)
 
 
 if __name__ == "__main__":

@@ -6,18 +6,22 @@
 //   CNB(k)  one thread per check copy: recompute the check node from the saved v2c_k (gathered at
 //           the cyclic shift), take dL/dc2v_{k+1} at the same addresses, and push it back through
 //           sign, clip/quantise (straight-through, closed interval), ReLU mask, learned weights
-//           (per-edge weight gradients: block reduction + one atomic per edge and block), |.|, and
+//           (per-edge weight gradients: per-workgroup partial sums, reduced at the end), |.|, and
 //           the min (routed to the first-index argmin of the others, as torch.min's backward) or
 //           the sum-product chain (tanh / product / atanh); writes dL/dv2c_k in place of v2c_k's
 //           addresses.
 //   VNB(k)  one thread per variable copy: dL/dc2v_k[e] = dL/dy_{k-1} (output clamp mask) +
 //           sum of dL/dv2c_k over the column's other edges; and the cumulative VN-weight chain
 //           xin_k = Q(xin_{k-1} * w_k) (straight-through masks, per-column weight gradients).
-// Gradient sums over the batch use fp32 atomics, so the last bits may vary from run to run
-// (tests use rtol 1e-4).
+// Weight gradients are summed over the batch without atomics: every workgroup writes its partial sum
+// per edge (column) and iteration into the workspace, and one reduction kernel at the end adds them
+// up in a fixed order (deterministic; thousands of same-address float atomics on a handful of cache
+// lines serialised in L2 and bounded both backward kernels before).
 #include <hip/hip_runtime.h>
 
-#include "nldpc_node.h"
+#include <cstdlib>
+
+#include "nldpc_fused.h"
 
 namespace nldpc {
 
@@ -31,8 +35,9 @@ struct VNBArgs {
     // cumulative VN weights (nullptr = no VN-weight gradient)
     const float* xa;
     const float* w_vn;     // [steps][N]
-    float* g_w_vn;         // [steps][N]
+    float* p_vn;           // [nb][N] per-workgroup partials of dL/dw_vn[step], or nullptr
     float* carry;          // [B][N][Z] dL/du_{p+1} * w_{p+1}
+    const float* xin_prev; // [B][N][Z] saved xin_{p-1} (the forward's value), or nullptr: recompute
     int32_t step;          // absolute VN step p of this iteration
     int32_t qbit;
 };
@@ -46,9 +51,9 @@ struct CNBArgs {
     const float* w_cn;    // [E] or nullptr
     const float* w_ucn;   // [E] or nullptr
     const float* bias;    // [E] or nullptr
-    float* g_w_cn;        // [E] or nullptr
-    float* g_w_ucn;       // [E] or nullptr
-    float* g_bias;        // [E] or nullptr
+    float* p_cn;          // [nb][E] per-workgroup partials of dL/dw_cn (this iteration), or nullptr
+    float* p_ucn;         // [nb][E] dL/dw_ucn partials, or nullptr
+    float* p_bias;        // [nb][E] dL/dbias partials, or nullptr
     const float* app;     // UCN hard-decision source (see CNArgs)
     const float* xa;
     const float* w_vn0;
@@ -56,9 +61,11 @@ struct CNBArgs {
     float lo, hi;
 };
 
-// Sum of one value over the workgroup, added once to *dst (lane 0 of wave 0).  Every thread of
-// the block must call it (uniform control flow).
-__device__ __forceinline__ void block_atomic_add(float v, float* dst, float* lds) {
+__device__ __forceinline__ int block_slot() { return blockIdx.x * gridDim.z + blockIdx.z; }
+
+// Sum of one value over the workgroup, stored by thread 0 into dst[block_slot() * width].  Every
+// thread of the block calls it (uniform control flow).
+__device__ __forceinline__ void block_partial(float v, float* dst, int width, float* lds) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     const int tid = threadIdx.y * blockDim.x + threadIdx.x;
     const int nw = (blockDim.x * blockDim.y + 63) >> 6;
@@ -67,21 +74,60 @@ __device__ __forceinline__ void block_atomic_add(float v, float* dst, float* lds
     if (tid == 0) {
         float s = 0.f;
         for (int w = 0; w < nw; ++w) s += lds[w];
-        if (s != 0.f) atomicAdd(dst, s);
+        dst[(int64_t)block_slot() * width] = s;
+    }
+}
+
+// Per-edge sums of up to NA gradient arrays over the workgroup: a wave reduction per edge, the
+// wave partials in LDS, ONE barrier, then one store per (array, edge) into dst[a][block_slot()][e].
+// Every thread of the block calls it (uniform control flow); d is block-uniform.
+constexpr int kMaxWaves = 8;
+template <int DC, int NA>
+__device__ __forceinline__ void block_edge_partials(float (&v)[NA][DC], int d, float* const (&dst)[NA], int E,
+                                                    float* lds /* [kMaxWaves][NA][DC] */) {
+    const int tid = threadIdx.y * blockDim.x + threadIdx.x;
+    const int wv = tid >> 6, nw = (blockDim.x * blockDim.y + 63) >> 6;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        if (!dst[a]) continue;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (k < d) {
+                float x = v[a][k];
+                for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+                if ((tid & 63) == 0) lds[(wv * NA + a) * DC + k] = x;
+            }
+        }
     }
     __syncthreads();
+    if (tid < NA * DC) {
+        const int a = tid / DC, k = tid - a * DC;
+        if (k < d && dst[a]) {
+            float s = 0.f;
+            for (int w = 0; w < nw; ++w) s += lds[(w * NA + a) * DC + k];
+            dst[a][(int64_t)block_slot() * E + k] = s;
+        }
+    }
+}
+
+// out[r][c] += sum over b of part[r][b][c]  (r < rows, c < width), in ascending b
+__global__ void reduce_partials(const float* __restrict__ part, int64_t rows, int64_t nb, int64_t width,
+                                float* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= rows * width) return;
+    const int64_t r = t / width, c = t - r * width;
+    const float* p = part + r * nb * width + c;
+    float s = 0.f;
+    for (int64_t b = 0; b < nb; ++b) s += p[b * width];
+    out[t] += s;
 }
 
 template <int DV, int KIND>
-__global__ __launch_bounds__(512) void vnb_kernel(VNBArgs a) {
-    __shared__ float red[8];
+__device__ __forceinline__ void vnb_body(const VNBArgs& a, const Geo& q, const int beg, const int d, float* red) {
     const int Z = a.g.Z, N = a.g.N, E = a.g.E;
-    const Geo q = geo(a.B, Z);
     const int v = q.ok ? q.v : 0, j = q.node;
     const int64_t b = q.ok ? q.b : 0;
     const int64_t idx = (b * N + j) * Z + v;
-    const int beg = a.g.col_ptr[j];
-    const int d = a.g.col_ptr[j + 1] - beg;
     const int64_t base = b * E;
 
     float gsum = 0.f;  // sum over the column of dL/dv2c_k = dL/dxin_k (direct part)
@@ -118,15 +164,19 @@ __global__ __launch_bounds__(512) void vnb_kernel(VNBArgs a) {
             if (k < d) gsum += g[k];
     }
 
-    if (a.g_w_vn) {  // block-uniform branch
+    if (a.p_vn) {  // block-uniform branch
         float contrib = 0.f;
         if (q.ok) {
             // recompute xin_{p-1} and u_p = xin_{p-1} * w_p
-            const float xav = a.xa[idx];
-            float xprev = xav;
-            for (int s = 0; s < a.step; ++s) {
-                xprev = fmul(xprev, a.w_vn[(int64_t)s * N + j]);
-                if (KIND == NLDPC_QMS) xprev = quantize(xprev, a.qbit);
+            float xprev;
+            if (a.xin_prev) {
+                xprev = a.xin_prev[idx];
+            } else {
+                xprev = a.xa[idx];
+                for (int s = 0; s < a.step; ++s) {
+                    xprev = fmul(xprev, a.w_vn[(int64_t)s * N + j]);
+                    if (KIND == NLDPC_QMS) xprev = quantize(xprev, a.qbit);
+                }
             }
             const float wp = a.w_vn[(int64_t)a.step * N + j];
             const float u = fmul(xprev, wp);
@@ -140,19 +190,15 @@ __global__ __launch_bounds__(512) void vnb_kernel(VNBArgs a) {
             contrib = du * xprev;
             a.carry[idx] = du * wp;
         }
-        block_atomic_add(contrib, a.g_w_vn + (int64_t)a.step * N + j, red);
+        block_partial(contrib, a.p_vn + j, N, red);
     }
 }
 
 template <int DC, int KIND, bool UCN>
-__global__ __launch_bounds__(512) void cnb_kernel(CNBArgs a) {
-    __shared__ float red[8];
+__device__ __forceinline__ void cnb_body(const CNBArgs& a, const Geo& q, const int beg, const int d, float* red) {
     const int Z = a.g.Z, E = a.g.E;
-    const Geo q = geo(a.B, Z);
-    const int h = q.ok ? q.v : 0, i = q.node;
+    const int h = q.ok ? q.v : 0;
     const int64_t b = q.ok ? q.b : 0;
-    const int beg = a.g.row_ptr[i];
-    const int d = a.g.row_ptr[i + 1] - beg;
     const int64_t base = b * E;
 
     int vv[DC];
@@ -172,194 +218,204 @@ __global__ __launch_bounds__(512) void cnb_kernel(CNBArgs a) {
         }
     }
     const float u = (UCN && q.ok) ? ucn_flag<DC, KIND>(a.g, beg, d, vv, b, a.app, a.xa, a.w_vn0, a.qbit) : 0.f;
-    CnCore<DC> core;
-    cn_core<DC, KIND>(m, d, a.qbit, a.lo, a.hi, core);
-
-    const QRange qr = q_range(a.qbit);
-    float gout[DC];  // dL/dx_output_0 per edge
-    float gw[DC], gu[DC], gb[DC];
+    float wc[DC], wu[DC], bb[DC], gm[DC], gw[DC], gu[DC], gb[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        gw[k] = gu[k] = gb[k] = 0.f;
-        gout[k] = 0.f;
-        if (k < d) {
-            const int e = beg + k;
-            const float x = core.out0[k];
-            const float wc = a.w_cn ? a.w_cn[e] : 1.f;
-            const float wu = a.w_ucn ? a.w_ucn[e] : 0.f;
-            const CnEpi r = cn_epilogue<KIND, UCN>(x, wc, wu, a.bias ? a.bias[e] : 0.f, u, a.w_cn != nullptr,
-                                                   a.w_ucn != nullptr, a.qbit, a.lo, a.hi);
-            const float s = signf_t(x), ax = fabsf(x);
-            float gabs;
-            if (KIND == NLDPC_NEURAL) {
-                const float ga = (gc[k] * s) * (r.x1 > 0.f ? 1.f : 0.f);
-                gw[k] = ga * ax;
-                gb[k] = ga;
-                gabs = ga * wc;
-            } else {
-                float g2 = gc[k] * s;
-                if (KIND == NLDPC_QMS) {
-                    if (qr.active) g2 *= in_range(r.x2, qr.lo, qr.hi);
-                } else {
-                    g2 *= in_range(r.x2, a.lo, a.hi);
-                }
-                const float g1 = g2 * (r.x1 > 0.f ? 1.f : 0.f);
-                if (!a.w_cn) {
-                    gabs = g1;
-                } else if (UCN && a.w_ucn) {
-                    const float g11 = g1 * (1.f - u), g12 = g1 * u;
-                    gw[k] = g11 * ax;
-                    gu[k] = g12 * ax;
-                    gabs = g11 * wc + g12 * wu;
-                } else {
-                    gw[k] = g1 * ax;
-                    gabs = g1 * wc;
-                }
-            }
-            gout[k] = gabs * s;
-        }
+        wc[k] = (k < d && a.w_cn) ? a.w_cn[beg + k] : 1.f;
+        wu[k] = (k < d && a.w_ucn) ? a.w_ucn[beg + k] : 0.f;
+        bb[k] = (k < d && a.bias) ? a.bias[beg + k] : 0.f;
     }
-
-    float gm[DC];
-    if (KIND == NLDPC_SP) {
-        float graw[DC];
-#pragma unroll
-        for (int l = 0; l < DC; ++l) graw[l] = 0.f;
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            if (k < d) {
-                float P = 1.f;
-#pragma unroll
-                for (int l = 0; l < DC; ++l)
-                    if (l < d && l != k) P = fmul(P, core.mq[l]);
-                const float Pc = clampf(P, -kSpClip, kSpClip);
-                // d(-2 atanh(P))/dP = -2 / (1 - P^2); clamp passes on the closed interval
-                const float gP = gout[k] * (-2.f / (1.f - Pc * Pc)) * in_range(P, -kSpClip, kSpClip);
-#pragma unroll
-                for (int l = 0; l < DC; ++l)
-                    if (l < d && l != k) graw[l] += gP * (P / core.mq[l]);  // torch.prod backward form
-            }
-        }
-#pragma unroll
-        for (int l = 0; l < DC; ++l) {
-            if (l < d) {
-                const float xc = clampf(m[l], a.lo, a.hi);
-                const float t = tanhf(fmul(-0.5f, xc));
-                gm[l] = graw[l] * (1.f - t * t) * -0.5f * in_range(m[l], a.lo, a.hi);
-            } else {
-                gm[l] = 0.f;
-            }
-        }
-    } else {
-        float gq[DC];
-#pragma unroll
-        for (int l = 0; l < DC; ++l) gq[l] = 0.f;
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            if (k < d) {
-                const int tgt = (k == core.idx1) ? core.idx2 : core.idx1;
-                const float gmag = gout[k] * core.sg[k];
-#pragma unroll
-                for (int l = 0; l < DC; ++l)
-                    if (l == tgt) gq[l] += gmag * signf_t(core.mq[l]);
-            }
-        }
-#pragma unroll
-        for (int l = 0; l < DC; ++l) {
-            float msk = 1.f;
-            if (KIND == NLDPC_QMS && qr.active) msk = in_range(m[l], qr.lo, qr.hi);
-            if (KIND == NLDPC_MS) msk = in_range(m[l], a.lo, a.hi);
-            gm[l] = gq[l] * msk;
-        }
-    }
+    cn_backward<DC, KIND, UCN>(m, gc, d, u, wc, wu, bb, a.w_cn != nullptr, a.w_ucn != nullptr, a.qbit, a.lo, a.hi, gm,
+                               gw, gu, gb);
     if (q.ok) {
 #pragma unroll
         for (int k = 0; k < DC; ++k)
             if (k < d) a.gv2c[(base + beg + k) * Z + vv[k]] = gm[k];
     }
-    // per-edge weight gradients: one block reduction per edge of the row
+    // per-edge weight gradients: wave reductions, one barrier, one partial per edge and block
+    float gacc[3][DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        if (k < d) {
-            if (a.g_w_cn) block_atomic_add(gw[k], a.g_w_cn + beg + k, red);
-            if (UCN && a.g_w_ucn) block_atomic_add(gu[k], a.g_w_ucn + beg + k, red);
-            if (KIND == NLDPC_NEURAL && a.g_bias) block_atomic_add(gb[k], a.g_bias + beg + k, red);
-        }
+        gacc[0][k] = gw[k];
+        gacc[1][k] = gu[k];
+        gacc[2][k] = gb[k];
     }
+    float* const dst[3] = {a.p_cn ? a.p_cn + beg : nullptr, (UCN && a.p_ucn) ? a.p_ucn + beg : nullptr,
+                           (KIND == NLDPC_NEURAL && a.p_bias) ? a.p_bias + beg : nullptr};
+    block_edge_partials<DC, 3>(gacc, d, dst, E, red);
 }
 
-template <int DV, int KIND>
+// Kernels: one switch on the workgroup-uniform degree, then a body with a compile-time degree
+// (deg_switch, nldpc_node.h).  The bodies hold barriers: every thread of a block takes the same case.
+template <int KIND, int MAXD>
+__global__ __launch_bounds__(512) void vnb_kernel(VNBArgs a) {
+    __shared__ float red[kMaxWaves];
+    const Geo q = geo(a.B, a.g.Z);
+    const int beg = a.g.col_ptr[q.node];
+    deg_switch<MAXD>(a.g.col_ptr[q.node + 1] - beg,
+                     [&](auto D, int d) { vnb_body<decltype(D)::value, KIND>(a, q, beg, d, red); });
+}
+
+template <int KIND, bool UCN, int MAXD>
+__global__ __launch_bounds__(512) void cnb_kernel(CNBArgs a) {
+    __shared__ float red[kMaxWaves * 3 * MAXD];
+    const Geo q = geo(a.B, a.g.Z);
+    const int beg = a.g.row_ptr[q.node];
+    deg_switch<MAXD>(a.g.row_ptr[q.node + 1] - beg,
+                     [&](auto D, int d) { cnb_body<decltype(D)::value, KIND, UCN>(a, q, beg, d, red); });
+}
+
+template <int KIND>
 static hipError_t launch_vnb(const VNBArgs& a, hipStream_t s) {
     dim3 grid, block;
     node_geometry(a.B, a.g.Z, a.g.N, grid, block);
     prof_start(PROF_VNB, s);
-    hipLaunchKernelGGL((vnb_kernel<DV, KIND>), grid, block, 0, s, a);
+    switch (deg_max_bucket(a.g.max_dv)) {
+        case 12: hipLaunchKernelGGL((vnb_kernel<KIND, 12>), grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL((vnb_kernel<KIND, 16>), grid, block, 0, s, a); break;
+        case 24: hipLaunchKernelGGL((vnb_kernel<KIND, 24>), grid, block, 0, s, a); break;
+        case 32: hipLaunchKernelGGL((vnb_kernel<KIND, 32>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((vnb_kernel<KIND, 64>), grid, block, 0, s, a); break;
+    }
     prof_stop(s);
     return hipGetLastError();
-}
-
-template <int KIND>
-static hipError_t vnb_dispatch(const VNBArgs& a, hipStream_t s) {
-    switch (deg_bucket(a.g.max_dv)) {
-        case 8: return launch_vnb<8, KIND>(a, s);
-        case 16: return launch_vnb<16, KIND>(a, s);
-        case 32: return launch_vnb<32, KIND>(a, s);
-        default: return launch_vnb<64, KIND>(a, s);
-    }
 }
 
 static hipError_t vnb_launch(int kind, const VNBArgs& a, hipStream_t s) {
     switch (kind) {
-        case NLDPC_NEURAL: return vnb_dispatch<NLDPC_NEURAL>(a, s);
-        case NLDPC_SP: return vnb_dispatch<NLDPC_SP>(a, s);
-        case NLDPC_MS: return vnb_dispatch<NLDPC_MS>(a, s);
-        default: return vnb_dispatch<NLDPC_QMS>(a, s);
+        case NLDPC_NEURAL: return launch_vnb<NLDPC_NEURAL>(a, s);
+        case NLDPC_SP: return launch_vnb<NLDPC_SP>(a, s);
+        case NLDPC_MS: return launch_vnb<NLDPC_MS>(a, s);
+        default: return launch_vnb<NLDPC_QMS>(a, s);
     }
 }
 
-template <int DC, int KIND, bool UCN>
+template <int KIND, bool UCN>
 static hipError_t launch_cnb(const CNBArgs& a, hipStream_t s) {
     dim3 grid, block;
     node_geometry(a.B, a.g.Z, a.g.M, grid, block);
     prof_start(PROF_CNB, s);
-    hipLaunchKernelGGL((cnb_kernel<DC, KIND, UCN>), grid, block, 0, s, a);
+    switch (deg_max_bucket(a.g.max_dc)) {
+        case 12: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 12>), grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 16>), grid, block, 0, s, a); break;
+        case 24: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 24>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 32>), grid, block, 0, s, a); break;
+    }
     prof_stop(s);
     return hipGetLastError();
 }
 
-template <int KIND, bool UCN>
-static hipError_t cnb_dispatch2(const CNBArgs& a, hipStream_t s) {
-    switch (deg_bucket(a.g.max_dc)) {
-        case 8: return launch_cnb<8, KIND, UCN>(a, s);
-        case 16: return launch_cnb<16, KIND, UCN>(a, s);
-        case 32: return launch_cnb<32, KIND, UCN>(a, s);
-        default: return hipErrorInvalidValue;
-    }
-}
-
 static hipError_t cnb_launch(int kind, bool ucn, const CNBArgs& a, hipStream_t s) {
     switch (kind) {
-        case NLDPC_NEURAL: return cnb_dispatch2<NLDPC_NEURAL, false>(a, s);
-        case NLDPC_SP: return ucn ? cnb_dispatch2<NLDPC_SP, true>(a, s) : cnb_dispatch2<NLDPC_SP, false>(a, s);
-        case NLDPC_MS: return ucn ? cnb_dispatch2<NLDPC_MS, true>(a, s) : cnb_dispatch2<NLDPC_MS, false>(a, s);
-        default: return ucn ? cnb_dispatch2<NLDPC_QMS, true>(a, s) : cnb_dispatch2<NLDPC_QMS, false>(a, s);
+        case NLDPC_NEURAL: return launch_cnb<NLDPC_NEURAL, false>(a, s);
+        case NLDPC_SP: return ucn ? launch_cnb<NLDPC_SP, true>(a, s) : launch_cnb<NLDPC_SP, false>(a, s);
+        case NLDPC_MS: return ucn ? launch_cnb<NLDPC_MS, true>(a, s) : launch_cnb<NLDPC_MS, false>(a, s);
+        default: return ucn ? launch_cnb<NLDPC_QMS, true>(a, s) : launch_cnb<NLDPC_QMS, false>(a, s);
     }
 }
 
 struct WorkLayout {
-    size_t gc_off, gv_off, carry_off, total;
+    size_t gc_off, gv_off, carry_off, pcn_off, pvn_off, total;
+    int64_t nb;  // workgroup slots along the batch (block_slot() range) of the node kernels
 };
 
-static WorkLayout work_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B) {
+// pcn: [3][T][nb][E] per-workgroup partials of dL/d(w_cn, w_ucn, bias); pvn: [vn_prefix+T][nb][N]
+static WorkLayout work_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T) {
     WorkLayout w;
     const size_t ez = (size_t)B * g->dev.E * g->dev.Z * sizeof(float);
     const size_t nz = (size_t)B * g->dev.N * g->dev.Z * sizeof(float);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    dim3 grid, block;
+    node_geometry(B, g->dev.Z, 1, grid, block);
+    w.nb = (int64_t)grid.x * grid.z;
     w.gc_off = 0;
     w.gv_off = al(ez);
     w.carry_off = w.gv_off + al(ez);
-    w.total = w.carry_off + (cfg->vn_cumulative ? al(nz) : 0);
+    w.pcn_off = w.carry_off + (cfg->vn_cumulative ? al(nz) : 0);
+    w.pvn_off = w.pcn_off + al((size_t)3 * T * w.nb * g->dev.E * sizeof(float));
+    w.total = w.pvn_off + (cfg->vn_cumulative ? al((size_t)(cfg->vn_prefix + T) * w.nb * g->dev.N * sizeof(float)) : 0);
     return w;
+}
+
+static hipError_t reduce_launch(const float* part, int64_t rows, int64_t nb, int64_t width, float* out, hipStream_t s) {
+    const int64_t n = rows * width;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(reduce_partials, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, rows, nb, width, out);
+    return hipGetLastError();
+}
+
+// ---- fused backward (register-resident kernels generated by gen_fused.py emit_bwd) ---------------
+static bool fused_bwd_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T) {
+    static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
+    if (disabled || (cfg->flags & NLDPC_FLAG_STREAM) || g->fused < 0) return false;
+    return !cfg->ucn && cfg->vn_prefix == 0 && T <= kFusedMaxT;
+}
+
+struct FusedWork {
+    size_t carry_off, pcn_off, pbias_off, pvn_off, total;
+    int64_t nslots;  // partial-sum slots per iteration: workgroups x waves per part
+};
+
+static FusedWork fused_work_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T) {
+    int n = 0;
+    const FusedSpec& f = fused_specs(&n)[g->fused];
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    FusedWork w;
+    w.nslots = (B + f.G - 1) / f.G * f.waves_per_part;
+    const size_t pe = (size_t)T * w.nslots * g->dev.E * sizeof(float);
+    w.carry_off = 0;
+    w.pcn_off = al(cfg->vn_cumulative ? (size_t)B * g->dev.N * g->dev.Z * sizeof(float) : 0);
+    w.pbias_off = w.pcn_off + al(pe);
+    w.pvn_off = w.pbias_off + (cfg->kind == NLDPC_NEURAL ? al(pe) : 0);
+    w.total = w.pvn_off + (cfg->vn_cumulative ? al((size_t)T * w.nslots * g->dev.N * sizeof(float)) : 0);
+    return w;
+}
+
+static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
+                          const float* w_cn, const float* bias, const float* w_vn, const float* const* grad_outs,
+                          const void* saved, float* g_w_cn, float* g_bias, float* g_w_vn, void* work,
+                          hipStream_t s) {
+    int n = 0;
+    const FusedSpec& f = fused_specs(&n)[g->fused];
+    const FusedWork W = fused_work_layout(g, cfg, B, T);
+    const SavedLayout SL = saved_layout(g, cfg, B, T);
+    const DevGraph& G = g->dev;
+    const char* sb = static_cast<const char*>(saved);
+    char* wb = static_cast<char*>(work);
+    FusedBwdArgs a{};
+    a.B = B;
+    a.T = T;
+    a.qbit = cfg->qbit;
+    a.lo = cfg->llr_lo;
+    a.hi = cfg->llr_hi;
+    a.xa = xa;
+    a.w_cn = w_cn;
+    a.bias = bias;
+    a.w_vn = (g_w_vn && cfg->vn_cumulative) ? w_vn : nullptr;  // the chain only feeds dL/dw_vn
+    a.sv2c = reinterpret_cast<const float*>(sb + SL.v2c_off);
+    a.symask = SL.has_ymask ? reinterpret_cast<const uint8_t*>(sb + SL.ymask_off) : nullptr;
+    a.sxin = SL.has_xin ? reinterpret_cast<const float*>(sb + SL.xin_off) : nullptr;
+    a.sv2c_stride = SL.v2c_stride;
+    a.symask_stride = SL.ymask_stride;
+    a.sxin_stride = SL.xin_stride;
+    a.p_cn = (g_w_cn && w_cn) ? reinterpret_cast<float*>(wb + W.pcn_off) : nullptr;
+    a.p_bias = (g_bias && bias && cfg->kind == NLDPC_NEURAL) ? reinterpret_cast<float*>(wb + W.pbias_off) : nullptr;
+    a.p_vn = a.w_vn ? reinterpret_cast<float*>(wb + W.pvn_off) : nullptr;
+    a.carry = a.w_vn ? reinterpret_cast<float*>(wb + W.carry_off) : nullptr;
+    a.nslots = W.nslots;
+    for (int k = 0; k < kFusedMaxT; ++k) a.gy.p[k] = k < T ? const_cast<float*>(grad_outs[k]) : nullptr;
+    void* args[] = {&a};
+    const int64_t blocks = (B + f.G - 1) / f.G;
+    prof_start(PROF_FUSED_BWD, s);
+    hipError_t e = hipLaunchKernel(f.bwd[cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args, 0, s);
+    prof_stop(s);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "fused backward launch");
+    if (a.p_cn) e = reduce_launch(a.p_cn, T, W.nslots, G.E, g_w_cn, s);
+    if (e == hipSuccess && a.p_bias) e = reduce_launch(a.p_bias, T, W.nslots, G.E, g_bias, s);
+    if (e == hipSuccess && a.p_vn) e = reduce_launch(a.p_vn, T, W.nslots, G.N, g_w_vn, s);
+    if (e != hipSuccess) return hip_fail(e, "reduce_partials launch");
+    return NLDPC_OK;
 }
 
 }  // namespace nldpc
@@ -371,7 +427,7 @@ extern "C" int nldpc_backward_workspace(const nldpc_graph* g, const nldpc_cfg* c
     int st = validate_cfg(g, cfg, B, T);
     if (st) return st;
     if (!bytes) return fail(NLDPC_EINVAL, "nldpc_backward_workspace: null output");
-    *bytes = work_layout(g, cfg, B).total;
+    *bytes = fused_bwd_eligible(g, cfg, T) ? fused_work_layout(g, cfg, B, T).total : work_layout(g, cfg, B, T).total;
     return NLDPC_OK;
 }
 
@@ -383,8 +439,10 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
     int st = validate_cfg(g, cfg, B, T);
     if (st) return st;
     if (!xa || !outs || !grad_outs || !saved || !work) return fail(NLDPC_EINVAL, "nldpc_backward: null argument");
-    const WorkLayout WL = work_layout(g, cfg, B);
-    if (work_bytes < WL.total) return fail(NLDPC_EINVAL, "nldpc_backward: workspace too small");
+    const bool fusedb = fused_bwd_eligible(g, cfg, T);
+    const WorkLayout WL = work_layout(g, cfg, B, T);
+    if (work_bytes < (fusedb ? fused_work_layout(g, cfg, B, T).total : WL.total))
+        return fail(NLDPC_EINVAL, "nldpc_backward: workspace too small");
     if (cfg->ucn && cfg->first_iter > 0 && !app_prev) return fail(NLDPC_EINVAL, "nldpc_backward: UCN needs app_prev");
     if (cfg->ucn)
         for (int k = 0; k + 1 < T; ++k)
@@ -392,14 +450,22 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
     if (g_w_vn && (!cfg->vn_cumulative || !w_vn)) return fail(NLDPC_EINVAL, "nldpc_backward: g_w_vn needs w_vn");
     DeviceGuard guard(g->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (fusedb) return fused_backward(g, cfg, B, T, xa, w_cn, bias, w_vn, grad_outs, saved, g_w_cn, g_bias, g_w_vn, work, s);
     const DevGraph& G = g->dev;
     const SavedLayout SL = saved_layout(g, cfg, B, T);
     const float* sv2c = reinterpret_cast<const float*>(static_cast<const char*>(saved) + SL.v2c_off);
     const uint8_t* smask = SL.has_ymask ? static_cast<const uint8_t*>(saved) + SL.ymask_off : nullptr;
+    const float* sxin = SL.has_xin ? reinterpret_cast<const float*>(static_cast<const char*>(saved) + SL.xin_off) : nullptr;
     char* wb = static_cast<char*>(work);
     float* gc = reinterpret_cast<float*>(wb + WL.gc_off);
     float* gv = reinterpret_cast<float*>(wb + WL.gv_off);
     float* carry = cfg->vn_cumulative ? reinterpret_cast<float*>(wb + WL.carry_off) : nullptr;
+    const int64_t nbE = WL.nb * G.E, nbN = WL.nb * G.N;
+    float* pcn = reinterpret_cast<float*>(wb + WL.pcn_off);  // [3][T][nb][E]
+    float* p_cn = (g_w_cn && w_cn) ? pcn : nullptr;
+    float* p_ucn = (g_w_ucn && cfg->ucn && w_ucn) ? pcn + (int64_t)T * nbE : nullptr;
+    float* p_bias = (g_bias && bias) ? pcn + 2 * (int64_t)T * nbE : nullptr;
+    float* p_vn = cfg->vn_cumulative ? reinterpret_cast<float*>(wb + WL.pvn_off) : nullptr;  // [P0+T][nb][N]
     const bool vn_grad = g_w_vn != nullptr;
     if (vn_grad) NLDPC_HIP_CHECK(hipMemsetAsync(carry, 0, (size_t)B * G.N * G.Z * sizeof(float), s));
     const int P0 = cfg->vn_prefix;
@@ -407,7 +473,7 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
     // dL/dc2v_T from the last output only
     {
         VNBArgs va{G, B, nullptr, grad_outs[T - 1],
-                   smask ? smask + (int64_t)(T - 1) * SL.ymask_stride : nullptr, gc, xa, w_vn, nullptr, carry, 0,
+                   smask ? smask + (int64_t)(T - 1) * SL.ymask_stride : nullptr, gc, xa, w_vn, nullptr, carry, nullptr, 0,
                    cfg->qbit};
         hipError_t e = vnb_launch(cfg->kind, va, s);
         if (e != hipSuccess) return hip_fail(e, "vnb_kernel launch");
@@ -423,9 +489,9 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
                    w_cn ? w_cn + (int64_t)k * G.E : nullptr,
                    (cfg->ucn && w_ucn) ? w_ucn + (int64_t)k * G.E : nullptr,
                    bias ? bias + (int64_t)k * G.E : nullptr,
-                   (g_w_cn && w_cn) ? g_w_cn + (int64_t)k * G.E : nullptr,
-                   (g_w_ucn && cfg->ucn && w_ucn) ? g_w_ucn + (int64_t)k * G.E : nullptr,
-                   (g_bias && bias) ? g_bias + (int64_t)k * G.E : nullptr,
+                   p_cn ? p_cn + (int64_t)k * nbE : nullptr,
+                   p_ucn ? p_ucn + (int64_t)k * nbE : nullptr,
+                   p_bias ? p_bias + (int64_t)k * nbE : nullptr,
                    app,
                    xa,
                    cfg->vn_cumulative ? w_vn : nullptr,
@@ -443,8 +509,9 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
                    k >= 1 ? gc : nullptr,
                    xa,
                    w_vn,
-                   vn_grad ? g_w_vn : nullptr,
+                   vn_grad ? p_vn + (int64_t)(P0 + k) * nbN : nullptr,
                    carry,
+                   (sxin && k >= 1) ? sxin + (int64_t)(k - 1) * SL.xin_stride : nullptr,
                    P0 + k,
                    cfg->qbit};
         e = vnb_launch(cfg->kind, va, s);
@@ -452,9 +519,17 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
     }
     // VN-weight chain through the steps applied before this call's first iteration
     for (int p = P0 - 1; vn_grad && p >= 0; --p) {
-        VNBArgs va{G, B, nullptr, nullptr, nullptr, nullptr, xa, w_vn, g_w_vn, carry, p, cfg->qbit};
+        VNBArgs va{G, B, nullptr, nullptr, nullptr, nullptr, xa, w_vn, p_vn + (int64_t)p * nbN, carry, nullptr, p,
+                   cfg->qbit};
         hipError_t e = vnb_launch(cfg->kind, va, s);
         if (e != hipSuccess) return hip_fail(e, "vnb_kernel launch");
     }
+    // the weight gradients: one fixed-order sum over the per-workgroup partials
+    hipError_t e = hipSuccess;
+    if (p_cn) e = reduce_launch(p_cn, T, WL.nb, G.E, g_w_cn, s);
+    if (e == hipSuccess && p_ucn) e = reduce_launch(p_ucn, T, WL.nb, G.E, g_w_ucn, s);
+    if (e == hipSuccess && p_bias) e = reduce_launch(p_bias, T, WL.nb, G.E, g_bias, s);
+    if (e == hipSuccess && vn_grad) e = reduce_launch(p_vn, P0 + T, WL.nb, G.N, g_w_vn, s);
+    if (e != hipSuccess) return hip_fail(e, "reduce_partials launch");
     return NLDPC_OK;
 }

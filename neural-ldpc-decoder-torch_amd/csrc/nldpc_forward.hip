@@ -29,6 +29,8 @@ struct VNArgs {
     uint8_t* ymask;      // [B][N][Z] clamp mask of the posterior (training) or nullptr
     const float* w_vn;   // [steps][N] cumulative VN weights (boosted) or nullptr
     int32_t n_vn_steps;  // number of cumulative weighting/quantisation steps for xin
+    const float* xin_prev;  // [B][N][Z] xin after n_vn_steps-1 steps (saved), or nullptr: from xa
+    float* xin_out;         // [B][N][Z] xin of this iteration (saved for the backward), or nullptr
     int32_t qbit;
     float lo, hi;
 };
@@ -51,15 +53,11 @@ struct CNArgs {
 };
 
 template <int DV, int KIND>
-__global__ __launch_bounds__(512) void vn_kernel(VNArgs a) {
+__device__ __forceinline__ void vn_body(const VNArgs& a, const Geo& q, const int beg, const int d) {
     const int Z = a.g.Z, N = a.g.N, E = a.g.E;
-    const Geo q = geo(a.B, Z);
-    if (!q.ok) return;
     const int v = q.v, j = q.node;
     const int64_t b = q.b;
     const int64_t idx = (b * N + j) * Z + v;
-    const int beg = a.g.col_ptr[j];
-    const int d = a.g.col_ptr[j + 1] - beg;
     const float xav = a.xa[idx];
     const int64_t base = b * E;
 
@@ -90,7 +88,14 @@ __global__ __launch_bounds__(512) void vn_kernel(VNArgs a) {
     }
 
     if (a.v2c) {
-        const float ch = vn_channel<KIND>(xav, a.w_vn, N, j, a.n_vn_steps, a.qbit);
+        float ch;
+        if (KIND != NLDPC_NEURAL && a.xin_prev) {  // one more step of the chain (same ops, same result)
+            ch = fmul(a.xin_prev[idx], a.w_vn[(int64_t)(a.n_vn_steps - 1) * N + j]);
+            if (KIND == NLDPC_QMS) ch = quantize(ch, a.qbit);
+        } else {
+            ch = vn_channel<KIND>(xav, a.w_vn, N, j, a.n_vn_steps, a.qbit);
+        }
+        if (KIND != NLDPC_NEURAL && a.xin_out) a.xin_out[idx] = ch;
         const float x0 = fadd(0.f, ch);  // xa_input @ W_skipconn2even
         float P = 0.f;                   // prefix ((0 + c0) + ... + c_{k-1})
 #pragma unroll
@@ -108,14 +113,10 @@ __global__ __launch_bounds__(512) void vn_kernel(VNArgs a) {
 }
 
 template <int DC, int KIND, bool UCN>
-__global__ __launch_bounds__(512) void cn_kernel(CNArgs a) {
+__device__ __forceinline__ void cn_body(const CNArgs& a, const Geo& q, const int beg, const int d) {
     const int Z = a.g.Z, E = a.g.E;
-    const Geo q = geo(a.B, Z);
-    if (!q.ok) return;
-    const int h = q.v, i = q.node;
+    const int h = q.v;
     const int64_t b = q.b;
-    const int beg = a.g.row_ptr[i];
-    const int d = a.g.row_ptr[i + 1] - beg;
     const int64_t base = b * E;
 
     int vv[DC];
@@ -146,62 +147,71 @@ __global__ __launch_bounds__(512) void cn_kernel(CNArgs a) {
     }
 }
 
-template <int DV, int KIND>
-static hipError_t launch_vn(const VNArgs& a, hipStream_t s) {
-    dim3 grid, block;
-    node_geometry(a.B, a.g.Z, a.g.N, grid, block);
-    hipLaunchKernelGGL((vn_kernel<DV, KIND>), grid, block, 0, s, a);
-    return hipGetLastError();
+template <int KIND, int MAXD>
+__global__ __launch_bounds__(512) void vn_kernel(VNArgs a) {
+    const Geo q = geo(a.B, a.g.Z);
+    if (!q.ok) return;
+    const int beg = a.g.col_ptr[q.node];
+    deg_switch<MAXD>(a.g.col_ptr[q.node + 1] - beg,
+                     [&](auto D, int d) { vn_body<decltype(D)::value, KIND>(a, q, beg, d); });
 }
 
-template <int DC, int KIND, bool UCN>
-static hipError_t launch_cn(const CNArgs& a, hipStream_t s) {
+template <int KIND, bool UCN, int MAXD>
+__global__ __launch_bounds__(512) void cn_kernel(CNArgs a) {
+    const Geo q = geo(a.B, a.g.Z);
+    if (!q.ok) return;
+    const int beg = a.g.row_ptr[q.node];
+    deg_switch<MAXD>(a.g.row_ptr[q.node + 1] - beg,
+                     [&](auto D, int d) { cn_body<decltype(D)::value, KIND, UCN>(a, q, beg, d); });
+}
+
+template <int KIND, int MAXD>
+static hipError_t vn_launch_k(const VNArgs& a, hipStream_t s) {
     dim3 grid, block;
-    node_geometry(a.B, a.g.Z, a.g.M, grid, block);
-    hipLaunchKernelGGL((cn_kernel<DC, KIND, UCN>), grid, block, 0, s, a);
+    node_geometry(a.B, a.g.Z, a.g.N, grid, block);
+    hipLaunchKernelGGL((vn_kernel<KIND, MAXD>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
 template <int KIND>
-static hipError_t dispatch_vn(int dv, const VNArgs& a, hipStream_t s) {
-    switch (deg_bucket(dv)) {
-        case 8: return launch_vn<8, KIND>(a, s);
-        case 16: return launch_vn<16, KIND>(a, s);
-        case 32: return launch_vn<32, KIND>(a, s);
-        default: return launch_vn<64, KIND>(a, s);
-    }
-}
-
-static hipError_t vn_launch(int kind, const VNArgs& a, hipStream_t s) {
-    switch (kind) {
-        case NLDPC_NEURAL: return dispatch_vn<NLDPC_NEURAL>(a.g.max_dv, a, s);
-        case NLDPC_SP: return dispatch_vn<NLDPC_SP>(a.g.max_dv, a, s);
-        case NLDPC_MS: return dispatch_vn<NLDPC_MS>(a.g.max_dv, a, s);
-        default: return dispatch_vn<NLDPC_QMS>(a.g.max_dv, a, s);
+static hipError_t vn_launch_m(const VNArgs& a, hipStream_t s) {
+    switch (deg_max_bucket(a.g.max_dv)) {
+        case 12: return vn_launch_k<KIND, 12>(a, s);
+        case 16: return vn_launch_k<KIND, 16>(a, s);
+        case 24: return vn_launch_k<KIND, 24>(a, s);
+        case 32: return vn_launch_k<KIND, 32>(a, s);
+        default: return vn_launch_k<KIND, 64>(a, s);
     }
 }
 
 template <int KIND, bool UCN>
-static hipError_t dispatch_cn2(const CNArgs& a, hipStream_t s) {
-    switch (deg_bucket(a.g.max_dc)) {
-        case 8: return launch_cn<8, KIND, UCN>(a, s);
-        case 16: return launch_cn<16, KIND, UCN>(a, s);
-        case 32: return launch_cn<32, KIND, UCN>(a, s);
-        default: return hipErrorInvalidValue;  // d_c > 32 needs a wider sign mask
+static hipError_t cn_launch_k(const CNArgs& a, hipStream_t s) {
+    dim3 grid, block;
+    node_geometry(a.B, a.g.Z, a.g.M, grid, block);
+    switch (deg_max_bucket(a.g.max_dc)) {
+        case 12: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 12>), grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 16>), grid, block, 0, s, a); break;
+        case 24: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 24>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 32>), grid, block, 0, s, a); break;
     }
+    return hipGetLastError();
 }
 
-template <int KIND>
-static hipError_t dispatch_cn(bool ucn, const CNArgs& a, hipStream_t s) {
-    return ucn ? dispatch_cn2<KIND, true>(a, s) : dispatch_cn2<KIND, false>(a, s);
+static hipError_t vn_launch(int kind, const VNArgs& a, hipStream_t s) {
+    switch (kind) {
+        case NLDPC_NEURAL: return vn_launch_m<NLDPC_NEURAL>(a, s);
+        case NLDPC_SP: return vn_launch_m<NLDPC_SP>(a, s);
+        case NLDPC_MS: return vn_launch_m<NLDPC_MS>(a, s);
+        default: return vn_launch_m<NLDPC_QMS>(a, s);
+    }
 }
 
 static hipError_t cn_launch(int kind, bool ucn, const CNArgs& a, hipStream_t s) {
     switch (kind) {
-        case NLDPC_NEURAL: return dispatch_cn2<NLDPC_NEURAL, false>(a, s);
-        case NLDPC_SP: return dispatch_cn<NLDPC_SP>(ucn, a, s);
-        case NLDPC_MS: return dispatch_cn<NLDPC_MS>(ucn, a, s);
-        default: return dispatch_cn<NLDPC_QMS>(ucn, a, s);
+        case NLDPC_NEURAL: return cn_launch_k<NLDPC_NEURAL, false>(a, s);
+        case NLDPC_SP: return ucn ? cn_launch_k<NLDPC_SP, true>(a, s) : cn_launch_k<NLDPC_SP, false>(a, s);
+        case NLDPC_MS: return ucn ? cn_launch_k<NLDPC_MS, true>(a, s) : cn_launch_k<NLDPC_MS, false>(a, s);
+        default: return ucn ? cn_launch_k<NLDPC_QMS, true>(a, s) : cn_launch_k<NLDPC_QMS, false>(a, s);
     }
 }
 
@@ -210,6 +220,7 @@ int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t 
     if (B <= 0 || T <= 0) return fail(NLDPC_EINVAL, "B and T must be positive");
     if (cfg->kind < NLDPC_SP || cfg->kind > NLDPC_NEURAL) return fail(NLDPC_EINVAL, "unknown decoder kind");
     if (g->dev.max_dc > 32) return fail(NLDPC_EUNSUPPORTED, "check degree above 32 is not supported");
+    if (g->dev.max_dv > 64) return fail(NLDPC_EUNSUPPORTED, "variable degree above 64 is not supported");
     if (cfg->kind == NLDPC_NEURAL && (cfg->ucn || cfg->vn_cumulative))
         return fail(NLDPC_EINVAL, "the Neural decoder has no UCN / VN weighting");
     if (B > 0x7FFFFFFFLL) return fail(NLDPC_EUNSUPPORTED, "batch too large for one launch (split the batch)");
@@ -227,19 +238,24 @@ SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     L.ymask_off = (v2c_bytes + 255) & ~(size_t)255;
     L.ymask_stride = B * NZ;  // bytes per iteration
     L.has_ymask = cfg->kind != NLDPC_NEURAL;
-    L.total = L.has_ymask ? L.ymask_off + (size_t)T * B * NZ : v2c_bytes;
+    const size_t end = L.has_ymask ? L.ymask_off + (size_t)T * B * NZ : v2c_bytes;
+    L.has_xin = cfg->vn_cumulative != 0;
+    L.xin_off = (end + 255) & ~(size_t)255;
+    L.xin_stride = B * NZ;  // floats per iteration
+    L.total = L.has_xin ? L.xin_off + (size_t)T * B * NZ * sizeof(float) : end;
     return L;
 }
 
 static bool fused_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T, bool saving) {
     static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
     if (disabled || (cfg->flags & NLDPC_FLAG_STREAM)) return false;
-    return g->fused >= 0 && !saving && !cfg->ucn && !cfg->c2v_in && T <= kFusedMaxT;
+    (void)saving;  // the SAVE kernels write what the backward needs
+    return g->fused >= 0 && !cfg->ucn && !cfg->c2v_in && T <= kFusedMaxT;
 }
 
 static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
                          const float* w_cn, const float* bias, const float* w_vn, float* const* outs, float* c2v,
-                         hipStream_t s) {
+                         void* saved, hipStream_t s) {
     int n = 0;
     const FusedSpec& f = fused_specs(&n)[g->fused];
     FusedArgs fa{};
@@ -255,10 +271,21 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     fa.hi = cfg->llr_hi;
     fa.c2v_out = (cfg->flags & NLDPC_FLAG_NO_STATE) ? nullptr : c2v;
     for (int k = 0; k < kFusedMaxT; ++k) fa.outs.p[k] = k < T ? outs[k] : nullptr;
+    if (saved) {
+        const SavedLayout SL = saved_layout(g, cfg, B, T);
+        char* sb = static_cast<char*>(saved);
+        fa.sv2c = reinterpret_cast<float*>(sb + SL.v2c_off);
+        fa.sv2c_stride = SL.v2c_stride;
+        fa.symask = SL.has_ymask ? reinterpret_cast<uint8_t*>(sb + SL.ymask_off) : nullptr;
+        fa.symask_stride = SL.ymask_stride;
+        fa.sxin = SL.has_xin ? reinterpret_cast<float*>(sb + SL.xin_off) : nullptr;
+        fa.sxin_stride = SL.xin_stride;
+    }
     void* args[] = {&fa};
     const int64_t blocks = (B + f.G - 1) / f.G;
     prof_start(PROF_FUSED, s);
-    hipError_t e = hipLaunchKernel(f.kernels[cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args, 0, s);
+    hipError_t e = hipLaunchKernel(f.kernels[saved ? 1 : 0][cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args,
+                                   0, s);
     prof_stop(s);
     if (e == hipSuccess) e = hipGetLastError();
     return e == hipSuccess ? NLDPC_OK : hip_fail(e, "fused kernel launch");
@@ -313,7 +340,7 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
     if (fused) {
         if (!c2v && !(cfg->flags & NLDPC_FLAG_NO_STATE))
             return fail(NLDPC_EINVAL, "nldpc_forward: c2v is required unless NLDPC_FLAG_NO_STATE");
-        return fused_forward(g, cfg, B, T, xa, w_cn, bias, w_vn, outs, c2v, s);
+        return fused_forward(g, cfg, B, T, xa, w_cn, bias, w_vn, outs, c2v, saved, s);
     }
     if (!c2v) return fail(NLDPC_EINVAL, "nldpc_forward: c2v is required by the streaming path");
     if (!v2c && !saved) return fail(NLDPC_EINVAL, "nldpc_forward: need v2c scratch or saved buffer");
@@ -321,6 +348,7 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
     const SavedLayout SL = saved_layout(g, cfg, B, T);
     float* saved_v2c = saved ? reinterpret_cast<float*>(static_cast<char*>(saved) + SL.v2c_off) : nullptr;
     uint8_t* saved_mask = (saved && SL.has_ymask) ? static_cast<uint8_t*>(saved) + SL.ymask_off : nullptr;
+    float* saved_xin = (saved && SL.has_xin) ? reinterpret_cast<float*>(static_cast<char*>(saved) + SL.xin_off) : nullptr;
     bool state_valid = cfg->c2v_in != 0;
     for (int k = 0; k < T; ++k) {
         float* v2c_k = saved_v2c ? saved_v2c + (int64_t)k * SL.v2c_stride : v2c;
@@ -333,6 +361,8 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
                   (k >= 1 && saved_mask) ? saved_mask + (int64_t)(k - 1) * SL.ymask_stride : nullptr,
                   cfg->vn_cumulative ? w_vn : nullptr,
                   cfg->vn_prefix + k + 1,
+                  (saved_xin && k >= 1) ? saved_xin + (int64_t)(k - 1) * SL.xin_stride : nullptr,
+                  saved_xin ? saved_xin + (int64_t)k * SL.xin_stride : nullptr,
                   cfg->qbit,
                   cfg->llr_lo,
                   cfg->llr_hi};
@@ -363,7 +393,8 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
     }
     if (outs[T - 1]) {
         VNArgs va{G, B, xa, c2v, nullptr, outs[T - 1],
-                  saved_mask ? saved_mask + (int64_t)(T - 1) * SL.ymask_stride : nullptr, nullptr, 0, cfg->qbit,
+                  saved_mask ? saved_mask + (int64_t)(T - 1) * SL.ymask_stride : nullptr, nullptr, 0, nullptr,
+                  nullptr, cfg->qbit,
                   cfg->llr_lo, cfg->llr_hi};
         prof_start(PROF_POST, s);
         hipError_t e = vn_launch(cfg->kind, va, s);

@@ -1,5 +1,5 @@
 // Register-resident fused decoder: shared declarations for the generated kernels
-// (gen_fused.py -> nldpc_fused_gen.hip) and their dispatcher in nldpc_forward.hip.
+// (gen_fused.py -> lib/gen/fused_*.hip) and their dispatcher in nldpc_forward.hip.
 #pragma once
 
 #include "nldpc_node.h"
@@ -23,6 +23,11 @@ struct FusedArgs {
     int32_t vn_prefix;
     float lo, hi;
     float* c2v_out;      // [B][E][Z] final message state, or nullptr
+    // what the backward needs (SAVE kernels only; SavedLayout in nldpc_internal.h)
+    float* sv2c;         // [T][B][E][Z] v2c of every iteration
+    uint8_t* symask;     // [T][B][N][Z] posterior clamp masks (Boosted), or nullptr
+    float* sxin;         // [T][B][N][Z] channel value xin of every iteration (cumulative VN weights), or nullptr
+    int64_t sv2c_stride, symask_stride, sxin_stride;  // elements per iteration
     OutPtrs outs;        // T posteriors [B][N][Z] (nullptr entries are skipped)
 };
 
@@ -41,6 +46,23 @@ __device__ __forceinline__ float bload(rsrc_t r, uint32_t vo, int so) {
 }
 __device__ __forceinline__ void bstore(rsrc_t r, uint32_t vo, int so, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, so, 0);
+}
+__device__ __forceinline__ void bstore8(rsrc_t r, uint32_t vo, int so, bool v) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, vo, so, 0);
+}
+
+// Channel value the VN adds.  With cumulative VN weights (Boosted, w_vn set) the registers hold xin
+// itself, advanced one step per iteration by chan_step (Boosted…py:325-337: xin <- Q(xin * w_t)),
+// so the chain is never re-run from xa; otherwise they hold xa and QMS quantises it (idempotent).
+template <int KIND>
+__device__ __forceinline__ float chan(float x, const FusedArgs& a) {
+    if (KIND == NLDPC_NEURAL || a.w_vn) return x;
+    return KIND == NLDPC_QMS ? quantize(x, a.qbit) : x;
+}
+template <int KIND>
+__device__ __forceinline__ float chan_step(float x, const FusedArgs& a, float w) {
+    x = fmul(x, w);
+    return KIND == NLDPC_QMS ? quantize(x, a.qbit) : x;
 }
 
 // posterior of one variable copy: Neural xa + P; Boosted clamp(Q(xa) + P) (Boosted…py:513-521)
@@ -61,10 +83,19 @@ __device__ __forceinline__ f2 posterior2(f2 xav, f2 P, const FusedArgs& a) {
     return f2{posterior<KIND>(xav.x, P.x, a), posterior<KIND>(xav.y, P.y, a)};
 }
 
+// Boosted posterior and its clamp mask (saved for the backward): in_range of the pre-clamp value
 template <int KIND>
-__device__ __forceinline__ f2 vn_channel2(f2 xa, const float* w_vn, int N, int j, int steps, int qbit) {
-    if (KIND == NLDPC_NEURAL) return xa;
-    return f2{vn_channel<KIND>(xa.x, w_vn, N, j, steps, qbit), vn_channel<KIND>(xa.y, w_vn, N, j, steps, qbit)};
+__device__ __forceinline__ float posterior_m(float xav, float P, const FusedArgs& a, bool& m) {
+    const float xo = (KIND == NLDPC_QMS) ? quantize(xav, a.qbit) : xav;
+    const float yp = fadd(xo, P);
+    m = yp >= a.lo && yp <= a.hi;
+    return clampf(yp, a.lo, a.hi);
+}
+
+template <int KIND>
+__device__ __forceinline__ f2 chan2(f2 x, const FusedArgs& a) {
+    if (KIND == NLDPC_NEURAL) return x;
+    return f2{chan<KIND>(x.x, a), chan<KIND>(x.y, a)};
 }
 
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
@@ -107,11 +138,53 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
     }
 }
 
+// Backward of the fused decoder (training): one workgroup per G codewords walks the iterations in
+// reverse with dL/dc2v in registers (same ownership as the forward's c2v), reading only the saved
+// v2c / clamp masks / xin and the incoming output gradients.  Weight gradients go to per-wave
+// partial sums [T][nslots][E|N] reduced afterwards (nldpc_backward.hip).  vn_prefix must be 0.
+struct FusedBwdArgs {
+    int64_t B;
+    int32_t T, qbit;
+    float lo, hi;
+    const float* xa;       // [B][N][Z]
+    const float* w_cn;     // [T][E] or nullptr
+    const float* bias;     // [T][E] (Neural) or nullptr
+    const float* w_vn;     // [T][N] or nullptr
+    const float* sv2c;     // saved [T][B][E][Z]
+    const uint8_t* symask; // saved [T][B][N][Z] or nullptr (Neural)
+    const float* sxin;     // saved [T][B][N][Z] or nullptr
+    int64_t sv2c_stride, symask_stride, sxin_stride;
+    float* p_cn;           // [T][nslots][E] or nullptr
+    float* p_bias;         // [T][nslots][E] or nullptr
+    float* p_vn;           // [T][nslots][N] or nullptr
+    float* carry;          // [B][N][Z] VN-chain carry (workspace; written before it is read)
+    int64_t nslots;
+    OutPtrs gy;            // T output gradients [B][N][Z] (nullptr = zero)
+};
+
+__device__ __forceinline__ uint32_t bload8(rsrc_t r, uint32_t vo, int so) {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, vo, so, 0);
+}
+// dL/dy of one variable copy through the Boosted output clamp (mask saved by the forward)
+template <int KIND>
+__device__ __forceinline__ float gy_masked(rsrc_t gr, rsrc_t mr, uint32_t vo, uint32_t vm, int so) {
+    const float g = bload(gr, vo, so);
+    if (KIND == NLDPC_NEURAL) return g;
+    return bload8(mr, vm, so >> 2) ? g : 0.f;
+}
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    return x;
+}
+
 struct FusedSpec {
     const char* tag;
     int32_t M, N, Z, E, G, threads;
     const int32_t* basegraph;  // [M*N]
-    void* kernels[4];          // indexed by nldpc_kind
+    void* kernels[2][4];       // [SAVE][nldpc_kind]
+    void* bwd[4];              // backward kernels [nldpc_kind]
+    int32_t waves_per_part;    // partial-sum slots per workgroup
 };
 
 const FusedSpec* fused_specs(int* n);

@@ -60,16 +60,18 @@ struct DeviceGuard {
 // Layout of the `saved` buffer nldpc_forward fills for nldpc_backward:
 //   v2c   [T][B][E][Z] fp32 variable-to-check messages of every iteration
 //   ymask [T][B][N][Z] uint8 clamp mask of every posterior (Boosted decoders only)
+//   xin   [T][B][N][Z] fp32 channel value xin_k each iteration used (cumulative VN weighting only),
+//         so neither direction re-runs the Q(x*w) chain from xa (O(T^2) over an unrolled forward)
 struct SavedLayout {
-    size_t v2c_off, ymask_off, total;
-    int64_t v2c_stride, ymask_stride;
-    bool has_ymask;
+    size_t v2c_off, ymask_off, xin_off, total;
+    int64_t v2c_stride, ymask_stride, xin_stride;
+    bool has_ymask, has_xin;
 };
 SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T);
 int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T);
 
 // benchmark instrumentation (nldpc_profile.cpp)
-enum ProfKind { PROF_VN = 0, PROF_CN = 1, PROF_POST = 2, PROF_FUSED = 3, PROF_VNB = 4, PROF_CNB = 5 };
+enum ProfKind { PROF_VN = 0, PROF_CN = 1, PROF_POST = 2, PROF_FUSED = 3, PROF_VNB = 4, PROF_CNB = 5, PROF_FUSED_BWD = 6 };
 bool prof_armed();
 void prof_start(int kind, hipStream_t s);
 void prof_stop(hipStream_t s);

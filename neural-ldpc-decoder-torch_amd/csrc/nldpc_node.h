@@ -57,6 +57,45 @@ inline void node_geometry(int64_t B, int Z, int nodes, dim3& grid, dim3& block) 
     grid = dim3((unsigned)((B + bt - 1) / bt), (unsigned)nodes, (unsigned)((Z + vt - 1) / vt));
 }
 
+// A node's degree is uniform over its workgroup (node-uniform grid), so the kernels switch on it once
+// and run a body templated on the exact degree: fully unrolled edge loops without per-edge
+// predicates, register arrays sized to the degree.  f(D, d): D = the compile-time array bound, d =
+// the degree as a value (a constant for the exact cases; the bucketed tail passes the runtime degree).
+template <int D>
+struct Deg {
+    static constexpr int value = D;
+};
+template <int MAXD, typename F>
+__device__ __forceinline__ void deg_switch(int d, F&& f) {
+    // only the cases up to MAXD (the launch's bucket of the graph's maximum degree) are instantiated,
+    // so the register allocation is that of the largest degree that can occur
+#define NLDPC_DEG_CASE(n) \
+    case n:                \
+        if constexpr (n <= MAXD) f(Deg<n>{}, n); \
+        break;
+    switch (d) {
+        NLDPC_DEG_CASE(1) NLDPC_DEG_CASE(2) NLDPC_DEG_CASE(3) NLDPC_DEG_CASE(4) NLDPC_DEG_CASE(5)
+        NLDPC_DEG_CASE(6) NLDPC_DEG_CASE(7) NLDPC_DEG_CASE(8) NLDPC_DEG_CASE(9) NLDPC_DEG_CASE(10)
+        NLDPC_DEG_CASE(11) NLDPC_DEG_CASE(12)
+        default:
+            if constexpr (MAXD > 12) {
+                if (d <= 16) {
+                    if constexpr (MAXD >= 16) f(Deg<16>{}, d);
+                } else if (d <= 24) {
+                    if constexpr (MAXD >= 24) f(Deg<24>{}, d);
+                } else if (d <= 32) {
+                    if constexpr (MAXD >= 32) f(Deg<32>{}, d);
+                } else {
+                    if constexpr (MAXD >= 64) f(Deg<64>{}, d);
+                }
+            }
+    }
+#undef NLDPC_DEG_CASE
+}
+
+// Bucket of a graph's maximum degree (the MAXD of deg_switch): 12, 16, 24, 32 or 64.
+inline int deg_max_bucket(int d) { return d <= 12 ? 12 : d <= 16 ? 16 : d <= 24 ? 24 : d <= 32 ? 32 : 64; }
+
 // xin of absolute VN step `steps-1`: Q(...Q(Q(xa*w0)*w1)...) (Boosted…py:325-337).
 template <int KIND>
 __device__ __forceinline__ float vn_channel(float xa, const float* w_vn, int N, int j, int steps, int qbit) {
@@ -222,6 +261,195 @@ __device__ __forceinline__ float ucn_flag(const DevGraph& g, int beg, int d, con
         }
     }
     return par ? 1.f : 0.f;
+}
+
+// Backward of one check copy of a degree-DC row (shared by the streaming cnb_kernel and the fused
+// backward kernels): from the gathered v2c inputs m and the incoming dL/dc2v gc, recompute the
+// forward (cn_core + cn_epilogue) and push the gradient back through sign, clip/quantise
+// (straight-through, closed interval), ReLU mask, learned weights, |.|, and the min (to the
+// first-index argmin of the others, as torch.min's backward) or the sum-product chain.
+// Out: gm = dL/dm per edge, gw/gu/gb = this copy's contributions to dL/dw_cn, dL/dw_ucn, dL/dbias.
+template <int DC, int KIND, bool UCN>
+__device__ __forceinline__ void cn_backward(const float (&m)[DC], const float (&gc)[DC], int d, float u,
+                                            const float (&wc)[DC], const float (&wu)[DC], const float (&bb)[DC],
+                                            bool has_w, bool has_u, int qbit, float lo, float hi, float (&gm)[DC],
+                                            float (&gw)[DC], float (&gu)[DC], float (&gb)[DC]) {
+    CnCore<DC> core;
+    cn_core<DC, KIND>(m, d, qbit, lo, hi, core);
+
+    const QRange qr = q_range(qbit);
+    float gout[DC];  // dL/dx_output_0 per edge
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        gw[k] = gu[k] = gb[k] = 0.f;
+        gout[k] = 0.f;
+        if (k < d) {
+            const float x = core.out0[k];
+            const CnEpi r = cn_epilogue<KIND, UCN>(x, wc[k], wu[k], bb[k], u, has_w, has_u, qbit, lo, hi);
+            const float s = signf_t(x), ax = fabsf(x);
+            float gabs;
+            if (KIND == NLDPC_NEURAL) {
+                const float ga = (gc[k] * s) * (r.x1 > 0.f ? 1.f : 0.f);
+                gw[k] = ga * ax;
+                gb[k] = ga;
+                gabs = ga * wc[k];
+            } else {
+                float g2 = gc[k] * s;
+                if (KIND == NLDPC_QMS) {
+                    if (qr.active) g2 *= in_range(r.x2, qr.lo, qr.hi);
+                } else {
+                    g2 *= in_range(r.x2, lo, hi);
+                }
+                const float g1 = g2 * (r.x1 > 0.f ? 1.f : 0.f);
+                if (!has_w) {
+                    gabs = g1;
+                } else if (UCN && has_u) {
+                    const float g11 = g1 * (1.f - u), g12 = g1 * u;
+                    gw[k] = g11 * ax;
+                    gu[k] = g12 * ax;
+                    gabs = g11 * wc[k] + g12 * wu[k];
+                } else {
+                    gw[k] = g1 * ax;
+                    gabs = g1 * wc[k];
+                }
+            }
+            gout[k] = gabs * s;
+        }
+    }
+
+    if (KIND == NLDPC_SP) {
+        float graw[DC];
+#pragma unroll
+        for (int l = 0; l < DC; ++l) graw[l] = 0.f;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (k < d) {
+                float P = 1.f;
+#pragma unroll
+                for (int l = 0; l < DC; ++l)
+                    if (l < d && l != k) P = fmul(P, core.mq[l]);
+                const float Pc = clampf(P, -kSpClip, kSpClip);
+                // d(-2 atanh(P))/dP = -2 / (1 - P^2); clamp passes on the closed interval
+                const float gP = gout[k] * (-2.f / (1.f - Pc * Pc)) * in_range(P, -kSpClip, kSpClip);
+#pragma unroll
+                for (int l = 0; l < DC; ++l)
+                    if (l < d && l != k) graw[l] += gP * (P / core.mq[l]);  // torch.prod backward form
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < DC; ++l) {
+            if (l < d) {
+                const float xc = clampf(m[l], lo, hi);
+                const float t = tanhf(fmul(-0.5f, xc));
+                gm[l] = graw[l] * (1.f - t * t) * -0.5f * in_range(m[l], lo, hi);
+            } else {
+                gm[l] = 0.f;
+            }
+        }
+    } else {
+        // torch.min backward: edge k's magnitude came from the first-index argmin of the OTHER
+        // edges, i.e. idx2 for k == idx1 and idx1 otherwise, so only two inputs receive gradient
+        float g_at1 = 0.f, g_at2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            if (k < d) {
+                const float gmag = gout[k] * core.sg[k];
+                if (k == core.idx1) g_at2 += gmag;
+                else g_at1 += gmag;
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < DC; ++l) {
+            float msk = 1.f;
+            if (KIND == NLDPC_QMS && qr.active) msk = in_range(m[l], qr.lo, qr.hi);
+            if (KIND == NLDPC_MS) msk = in_range(m[l], lo, hi);
+            const float gl = l == core.idx1 ? g_at1 : (l == core.idx2 ? g_at2 : 0.f);
+            gm[l] = (gl * signf_t(core.mq[l])) * msk;
+        }
+    }
+}
+
+// Register-light min-sum backward of one check copy (MS / QMS / Neural) for the fused backward
+// kernels: cn_backward's arithmetic (same operations, same order, same results) restructured into
+// three passes over the edges so that only the two minima and per-edge bit masks stay live between
+// them.  load_m(k) gives edge k's v2c input; lds[k * stride] holds dL/dc2v on entry and receives
+// dL/dv2c.  gwa / gba accumulate this copy's dL/dw_cn and dL/dbias contributions.
+template <int DC, int KIND, typename LoadM>
+__device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride, const float (&wc)[DC],
+                                          const float (&bb)[DC], bool has_w, int qbit, float lo, float hi,
+                                          float (&gwa)[DC], float (&gba)[DC]) {
+    const QRange qr = q_range(qbit);
+    float min1 = kMaskMag, min2 = kMaskMag;
+    int idx1 = -1, idx2 = -1;
+    uint32_t npos = 0, posm = 0, negm = 0, mskm = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {  // pass 1: conditioned inputs, minima, signs, STE masks
+        float x = load_m(k);
+        bool msk = true;
+        if (KIND == NLDPC_QMS && qr.active) msk = x >= qr.lo && x <= qr.hi;
+        if (KIND == NLDPC_MS) msk = x >= lo && x <= hi;
+        if (KIND == NLDPC_QMS) x = quantize(x, qbit);
+        if (KIND == NLDPC_MS) x = clampf(x, lo, hi);
+        if (KIND != NLDPC_NEURAL) x = fadd(x, fmul(kZeroFix, (fabsf(x) > 0.f) ? 0.f : 1.f));
+        const float ax = fabsf(x);
+        const uint32_t pos = x > 0.f;
+        npos ^= pos;
+        posm |= pos << k;
+        negm |= (uint32_t)(x < 0.f) << k;
+        mskm |= (uint32_t)msk << k;
+        if (ax > 0.f) {
+            if (ax < min1) {
+                min2 = min1;
+                idx2 = idx1;
+                min1 = ax;
+                idx1 = k;
+            } else if (ax < min2) {
+                min2 = ax;
+                idx2 = k;
+            }
+        }
+    }
+    float g_at1 = 0.f, g_at2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {  // pass 2: epilogue backward per edge (cn_backward's formulas)
+        float mag = (k == idx1) ? min2 : min1;
+        if (KIND != NLDPC_NEURAL) mag = (mag > kZeroFix) ? mag : fadd(mag, -kZeroFix);
+        const float sgn = ((npos ^ (posm >> k)) & 1u) ? 1.f : -1.f;
+        const float x = fmul(mag, sgn);
+        const CnEpi r = cn_epilogue<KIND, false>(x, wc[k], 0.f, bb[k], 0.f, has_w, false, qbit, lo, hi);
+        const float s = signf_t(x), ax = fabsf(x);
+        const float gc = lds[k * stride];
+        float gabs;
+        if (KIND == NLDPC_NEURAL) {
+            const float ga = (gc * s) * (r.x1 > 0.f ? 1.f : 0.f);
+            gwa[k] += ga * ax;
+            gba[k] += ga;
+            gabs = ga * wc[k];
+        } else {
+            float g2 = gc * s;
+            if (KIND == NLDPC_QMS) {
+                if (qr.active) g2 *= in_range(r.x2, qr.lo, qr.hi);
+            } else {
+                g2 *= in_range(r.x2, lo, hi);
+            }
+            const float g1 = g2 * (r.x1 > 0.f ? 1.f : 0.f);
+            if (!has_w) {
+                gabs = g1;
+            } else {
+                gwa[k] += g1 * ax;
+                gabs = g1 * wc[k];
+            }
+        }
+        const float gmag = (gabs * s) * sgn;
+        if (k == idx1) g_at2 += gmag;
+        else g_at1 += gmag;
+    }
+#pragma unroll
+    for (int l = 0; l < DC; ++l) {  // pass 3: the two argmins receive the gradient
+        const float gl = l == idx1 ? g_at1 : (l == idx2 ? g_at2 : 0.f);
+        const float smq = ((posm >> l) & 1u) ? 1.f : (((negm >> l) & 1u) ? -1.f : 0.f);
+        lds[l * stride] = (gl * smq) * (((mskm >> l) & 1u) ? 1.f : 0.f);
+    }
 }
 
 }  // namespace nldpc

@@ -63,7 +63,7 @@ extern "C" int nldpc_profile_begin(int32_t capacity) {
 }
 
 // ms[k], count[k] for kind k in 0..nkinds-1 (0 = VN, 1 = CN, 2 = posterior, 3 = fused, 4 = VN backward,
-// 5 = CN backward)
+// 5 = CN backward, 6 = fused backward)
 extern "C" int nldpc_profile_end(int32_t nkinds, float* ms, int32_t* count) {
     g_prof.armed = false;
     for (int k = 0; k < nkinds; ++k) {

@@ -148,8 +148,78 @@ def test_fast_path_selection():
     L = _lib.lib()
     for bg, Z, want in ((BG2, 384, 1), (BG2, 16, 1), (WIMAX, 24, 1), (BG2, 64, 0)):
         g = _graph(bg, Z)
-        for save, ucn, exp in ((0, False, want), (1, False, 0), (0, True, 0)):
+        for save, ucn, exp in ((0, False, want), (1, False, want), (0, True, 0)):
             cfg = DecodeCfg(KIND_NEURAL if not ucn else 1, ucn=ucn).c_struct(False)
             out = ctypes.c_int32(-1)
             _lib.check(L.nldpc_fast_path(g.handle(DEV), ctypes.byref(cfg), 4, 20, save, ctypes.byref(out)))
             assert out.value == exp, (Z, save, ucn)
+
+
+@pytest.mark.parametrize("Z,B", [(384, 3), (16, 21)])
+@pytest.mark.parametrize("kind,prefix", [(0, 0), (1, 0), (2, 0), (2, 2), (3, 0)])
+def test_saved_activations_fused_equal_stream(kind, prefix, Z, B):
+    """Training forward: the fused kernel's SAVE variant writes exactly what the streaming kernels
+    write for the backward (every iteration's v2c, the posterior clamp masks, the xin chain), and the
+    same outputs.  Z=16 packs 16 codewords per workgroup (B=21: a partial last workgroup)."""
+    from nldpc.decode import KIND_NEURAL, DecodeCfg, decode
+    T = 5
+    g = _graph(BG2, Z)
+    gen = torch.Generator().manual_seed(100 * kind + Z + prefix)
+    x = (2 * (-1 + 0.9 * torch.randn(B, 52, Z, generator=gen)) / 0.81).float().to(DEV)
+    if kind == KIND_NEURAL:
+        kw = dict(w_cn=(torch.rand(T, g.E, generator=gen) * 1.2).to(DEV),
+                  bias=(torch.randn(T, g.E, generator=gen) * 0.1).to(DEV))
+    else:
+        kw = dict(w_cn=(0.5 + torch.rand(T, 42, generator=gen))[:, torch.as_tensor(g.chk)].contiguous().to(DEV),
+                  w_vn=(0.8 + 0.4 * torch.rand(prefix + T, 52, generator=gen)).to(DEV))
+    res = {}
+    for path in ("stream", "fused"):
+        cfg = DecodeCfg(kind=kind, qbit=5, vn_cumulative=kind != KIND_NEURAL, vn_prefix=prefix, path=path)
+        res[path] = decode(g, cfg, x, T, save=True, **kw)
+    assert torch.equal(res["stream"][0], res["fused"][0])
+    assert torch.equal(res["stream"][1], res["fused"][1])
+    # sections of the saved buffer (SavedLayout, nldpc_internal.h); the alignment gaps are not written
+    al = lambda n: (n + 255) // 256 * 256  # noqa: E731
+    v2c = T * B * g.E * Z * 4
+    secs = [(0, v2c)]
+    end = v2c
+    if kind != KIND_NEURAL:
+        secs.append((al(v2c), T * B * 52 * Z))
+        end = al(v2c) + T * B * 52 * Z
+        secs.append((al(end), T * B * 52 * Z * 4))
+    for name, (off, n) in zip(("v2c", "ymask", "xin"), secs):
+        assert torch.equal(res["stream"][2][off:off + n], res["fused"][2][off:off + n]), f"saved {name} differs"
+
+
+@pytest.mark.parametrize("Z,B", [(384, 3), (16, 21)])
+@pytest.mark.parametrize("kind", [1, 2, 3])
+def test_fused_backward_equals_stream(kind, Z, B):
+    """Training backward: the register-resident backward kernel gives the streaming kernels' weight
+    gradients (same arithmetic; only the order of the batch sums differs)."""
+    from nldpc.decode import KIND_NEURAL, DecodeCfg, decode, decode_backward
+    T = 5
+    g = _graph(BG2, Z)
+    gen = torch.Generator().manual_seed(7 * kind + Z)
+    x = (2 * (-1 + 0.9 * torch.randn(B, 52, Z, generator=gen)) / 0.81).float().to(DEV)
+    if kind == KIND_NEURAL:
+        kw = dict(w_cn=(torch.rand(T, g.E, generator=gen) * 1.2).to(DEV),
+                  bias=(torch.randn(T, g.E, generator=gen) * 0.1).to(DEV))
+        need = (True, False, True, False)
+    else:
+        kw = dict(w_cn=(0.5 + torch.rand(T, 42, generator=gen))[:, torch.as_tensor(g.chk)].contiguous().to(DEV),
+                  w_vn=(0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV))
+        need = (True, False, False, True)
+    go = [(torch.randn(B, 52 * Z, generator=gen) * 1e-2).to(DEV) for _ in range(T)]
+    res = {}
+    for path in ("stream", "fused"):
+        cfg = DecodeCfg(kind=kind, qbit=5, vn_cumulative=kind != KIND_NEURAL, path=path)
+        outs, _, saved = decode(g, cfg, x, T, save=True, **kw)
+        res[path] = decode_backward(g, cfg, x, T, go, list(outs.unbind(0)), saved, need=need, **kw)
+    n = 0
+    for a, b in zip(res["stream"], res["fused"]):
+        assert (a is None) == (b is None)
+        if a is not None:
+            a, b = a.cpu().numpy(), b.cpu().numpy()
+            np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-5 * max(np.abs(a).max(), 1e-12))
+            n += 1
+    assert n == 2
