@@ -139,6 +139,25 @@ int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_
 int nldpc_ber_count(const float* llr, const uint8_t* y, int64_t B, int64_t L, int32_t convention,
                     int64_t* counts, void* stream);
 
+/* ---- multi-iteration BCE loss (config 5's training loss): replaces LDPCDecoderLoss.forward with
+ *      LossType.BCE over a list of outputs and one label tensor
+ *      (src/boosted_neural_ldpc_decoder/LDPCDecoderLoss.py:70-108, binary_cross_entropy_with_logits
+ *      per term) and its autograd backward, in one pass over the T outputs instead of a chain of
+ *      elementwise ops per term.
+ *   logits   host array of K device pointers, each [n] fp32 (K <= 64)
+ *   coef     host [K]: weight of term k (etha^c_k / sum_k etha^c_k)
+ *   target   [n] fp32 labels shared by every term, or NULL (all zero)
+ *   loss     device fp32 scalar out: sum_k coef[k] * mean_i bce(logits[k][i], target[i]), with
+ *            bce(x, t) = (1 - t) * x - log_sigmoid(x) (fp32 terms, fp64 fixed-order sums)
+ *   work     device scratch of nldpc_bce_workspace() bytes
+ *   grads    (nldpc_bce_grad) K device pointers [n]: grads[k][i] = (*gseed) * coef[k] / n *
+ *            (sigmoid(logits[k][i]) - target[i]); gseed is a device fp32 scalar (dL/dloss) */
+int nldpc_bce_workspace(int64_t n, int32_t K, size_t* bytes);
+int nldpc_bce_loss(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
+                   float* loss, void* work, size_t work_bytes, void* stream);
+int nldpc_bce_grad(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
+                   const float* gseed, float* const* grads, void* stream);
+
 /* ---- synthetic AWGN channel (the step before the path; replaces the all-zero branch of
  *      AWGNPassedDatagen, boosted.../AWGNPassedDatagen.py:75-134, generated on the device):
  *   xa[b][n] = 2*(-1 + sigma*g)/sigma^2 with g ~ N(0,1) from Philox-4x32-10(seed) at counter

@@ -1,6 +1,8 @@
 // The steps either side of the decode path:
 //   nldpc_awgn_llr   synthetic BPSK/AWGN channel LLRs generated in HBM (Philox-4x32-10 + Box-Muller)
 //   nldpc_ber_count  fused bit/frame error counting of a posterior (Functions.evaluate_ber_fer)
+//   nldpc_bce_loss / nldpc_bce_grad  the multi-iteration BCE training loss and its gradient
+//                    (LDPCDecoderLoss.py:70-108), one pass over all T outputs each
 #include <hip/hip_runtime.h>
 
 #include "nldpc_internal.h"
@@ -87,9 +89,115 @@ __global__ __launch_bounds__(256) void ber_kernel(const float* llr, const uint8_
     }
 }
 
+// ---------------------------------------------------------------- multi-iteration BCE loss
+constexpr int kBceMaxK = 64;
+constexpr int kBceBlocks = 1024;
+struct BceArgs {
+    const float* x[kBceMaxK];
+    float coef[kBceMaxK];
+    int32_t K;
+};
+
+// torch.nn.functional.binary_cross_entropy_with_logits term: (1 - t) * x - log_sigmoid(x)
+__device__ __forceinline__ float bce_term(float x, float t) {
+    const float ls = fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
+    return (1.f - t) * x - ls;
+}
+
+__global__ __launch_bounds__(256) void bce_loss_kernel(BceArgs a, const float* __restrict__ target, int64_t n,
+                                                       double* __restrict__ part) {
+    __shared__ double red[4];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float t = target ? target[i] : 0.f;
+        float s = 0.f;
+        for (int k = 0; k < a.K; ++k) s += a.coef[k] * bce_term(a.x[k][i], t);
+        acc += (double)s;
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(64) void bce_finish_kernel(const double* __restrict__ part, int nb, int64_t n,
+                                                        float* __restrict__ loss, int accumulate) {
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nb; b += 64) s += part[b];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (threadIdx.x == 0) {
+        const float v = (float)(s / (double)n);
+        *loss = accumulate ? *loss + v : v;
+    }
+}
+
+__global__ __launch_bounds__(256) void bce_grad_kernel(BceArgs a, const float* __restrict__ target, int64_t n,
+                                                       const float* __restrict__ gseed, BceArgs g) {
+    const float scale = *gseed / (float)n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float t = target ? target[i] : 0.f;
+        for (int k = 0; k < a.K; ++k) {
+            const float sg = 1.f / (1.f + expf(-a.x[k][i]));
+            const_cast<float*>(g.x[k])[i] = (scale * a.coef[k]) * (sg - t);
+        }
+    }
+}
+
 }  // namespace nldpc
 
 using namespace nldpc;
+
+extern "C" int nldpc_bce_workspace(int64_t n, int32_t K, size_t* bytes) {
+    if (!bytes || n <= 0 || K <= 0) return fail(NLDPC_EINVAL, "nldpc_bce_workspace: bad argument");
+    *bytes = kBceBlocks * sizeof(double);
+    return NLDPC_OK;
+}
+
+static int bce_blocks(int64_t n) {
+    const int64_t b = (n + 255) / 256;
+    return (int)(b < kBceBlocks ? b : kBceBlocks);
+}
+
+extern "C" int nldpc_bce_loss(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
+                              float* loss, void* work, size_t work_bytes, void* stream) {
+    if (!logits || !coef || !loss || !work || n <= 0 || K <= 0) return fail(NLDPC_EINVAL, "nldpc_bce_loss: bad argument");
+    if (work_bytes < kBceBlocks * sizeof(double)) return fail(NLDPC_EINVAL, "nldpc_bce_loss: workspace too small");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nb = bce_blocks(n);
+    for (int k0 = 0; k0 < K; k0 += kBceMaxK) {  // groups of up to 64 terms, accumulated into *loss
+        BceArgs a{};
+        a.K = K - k0 < kBceMaxK ? K - k0 : kBceMaxK;
+        for (int k = 0; k < a.K; ++k) {
+            if (!logits[k0 + k]) return fail(NLDPC_EINVAL, "nldpc_bce_loss: null logits");
+            a.x[k] = logits[k0 + k];
+            a.coef[k] = coef[k0 + k];
+        }
+        double* part = static_cast<double*>(work);
+        hipLaunchKernelGGL(bce_loss_kernel, dim3(nb), dim3(256), 0, s, a, target, n, part);
+        hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(64), 0, s, part, nb, n, loss, k0 > 0 ? 1 : 0);
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NLDPC_OK : hip_fail(e, "bce_loss_kernel launch");
+}
+
+extern "C" int nldpc_bce_grad(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
+                              const float* gseed, float* const* grads, void* stream) {
+    if (!logits || !coef || !gseed || !grads || n <= 0 || K <= 0) return fail(NLDPC_EINVAL, "nldpc_bce_grad: bad argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    for (int k0 = 0; k0 < K; k0 += kBceMaxK) {
+        BceArgs a{}, g{};
+        a.K = g.K = K - k0 < kBceMaxK ? K - k0 : kBceMaxK;
+        for (int k = 0; k < a.K; ++k) {
+            if (!logits[k0 + k] || !grads[k0 + k]) return fail(NLDPC_EINVAL, "nldpc_bce_grad: null pointer");
+            a.x[k] = logits[k0 + k];
+            a.coef[k] = coef[k0 + k];
+            g.x[k] = grads[k0 + k];
+        }
+        hipLaunchKernelGGL(bce_grad_kernel, dim3(bce_blocks(n) * 4), dim3(256), 0, s, a, target, n, gseed, g);
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NLDPC_OK : hip_fail(e, "bce_grad_kernel launch");
+}
 
 extern "C" int nldpc_awgn_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,
                               int32_t qbit, void* stream) {

@@ -4,7 +4,8 @@ loss = sum_k etha^c_k * L(outputs[k], expected[k]) / sum_k etha^c_k, then the ba
 L = BCE-with-logits (LossType.BCE), sigmoid(LLR) (SoftBEROnAllZero) or a straight-through frame-error
 indicator (FEROnAllZero).  Terms are accumulated from the last output to the first, as in the
 reference.  This is the backward seed of config 5; its gradient w.r.t. each output is what
-nldpc_backward consumes.
+nldpc_backward consumes.  On ROCm tensors the BCE over a list of outputs with one label tensor (the
+training script's call) runs as one fused HIP pass per direction (nldpc.loss.bce_multi).
 """
 from typing import Optional
 
@@ -13,6 +14,7 @@ import torch.nn as nn
 
 from boosted_neural_ldpc_decoder.Functions import Functions
 from boosted_neural_ldpc_decoder.struct.LossType import LossType
+from nldpc.loss import bce_multi
 
 
 class LDPCDecoderLoss(nn.Module):
@@ -43,6 +45,18 @@ class LDPCDecoderLoss(nn.Module):
             raise ValueError("Invalid coeff_param provided to LDPCDecoderLoss. Must be an integer when outputs is a "
                              "single torch.Tensor.")
         n = 1 if single else len(outputs)
+        if (self.loss_type == LossType.BCE and listed and expected.is_cuda and all(
+                isinstance(o, torch.Tensor) and o.is_cuda and o.shape == expected.shape for o in outputs)):
+            # device path: every term in one HIP pass (nldpc.loss); same sum, fixed-order fp64 reduction
+            ws = []
+            for k in range(n):
+                c = 1
+                if coeff_param is not None:
+                    c = coeff_param[k] if isinstance(coeff_param, list) else coeff_param
+                ws.append(pow(self.etha, c))
+            norm = sum(ws)
+            coef = [w / norm for w in ws] if norm > 0 else ws
+            return 1.0 * bce_multi(outputs, expected, coef)
         total, norm = 0, 0
         for k in reversed(range(n)):
             actual = outputs if single else outputs[k]

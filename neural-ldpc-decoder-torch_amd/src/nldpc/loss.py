@@ -1,0 +1,58 @@
+"""Multi-iteration BCE training loss on the device (config 5): the LossType.BCE branch of
+LDPCDecoderLoss.forward over a list of decoder outputs and one label tensor
+(src/boosted_neural_ldpc_decoder/LDPCDecoderLoss.py:70-108) as two HIP passes (nldpc_bce_loss /
+nldpc_bce_grad) instead of a chain of per-term elementwise ops and reductions."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+class BCEMultiFn(torch.autograd.Function):
+    """loss = sum_k coef[k] * mean(bce_with_logits(outputs[k], target)); coef already normalised."""
+
+    @staticmethod
+    def forward(ctx, target, coef, *outputs):
+        L = _lib.lib()
+        dev = outputs[0].device
+        n = outputs[0].numel()
+        xs = [o.detach().to(torch.float32).contiguous() for o in outputs]
+        t = target.detach().to(torch.float32).contiguous()
+        K = len(xs)
+        c = (ctypes.c_float * K)(*[float(v) for v in coef])
+        nb = ctypes.c_size_t(0)
+        _lib.check(L.nldpc_bce_workspace(n, K, ctypes.byref(nb)), "nldpc_bce_workspace")
+        work = torch.empty((int(nb.value),), dtype=torch.uint8, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        px, keep = _lib.ptr_array(xs)
+        st = L.nldpc_bce_loss(px, K, c, _lib.ptr(t), n, _lib.ptr(loss), _lib.ptr(work), int(work.numel()),
+                              _lib.stream_of(dev))
+        del keep
+        _lib.check(st, "nldpc_bce_loss")
+        ctx.coef = [float(v) for v in coef]
+        ctx.save_for_backward(t, *xs)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        t, *xs = ctx.saved_tensors
+        L = _lib.lib()
+        dev = xs[0].device
+        K, n = len(xs), xs[0].numel()
+        grads = [torch.empty_like(x) for x in xs]
+        c = (ctypes.c_float * K)(*ctx.coef)
+        gs = g.detach().to(torch.float32).reshape(()).contiguous()
+        px, k1 = _lib.ptr_array(xs)
+        pg, k2 = _lib.ptr_array(grads)
+        st = L.nldpc_bce_grad(px, K, c, _lib.ptr(t), n, _lib.ptr(gs), pg, _lib.stream_of(dev))
+        del k1, k2
+        _lib.check(st, "nldpc_bce_grad")
+        return (None, None, *grads)
+
+
+def bce_multi(outputs, target, coef):
+    """Differentiable multi-term BCE-with-logits on ROCm tensors (see BCEMultiFn)."""
+    return BCEMultiFn.apply(target, list(coef), *outputs)

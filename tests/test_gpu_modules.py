@@ -166,3 +166,29 @@ def test_awgn_llr_statistics_and_sharding():
     assert abs(noise.mean().item()) < 0.01 and abs(noise.std().item() - 1) < 0.01
     other = awgn_llr(B, N, Z, sigma, seed=12, device=DEV)
     assert not torch.equal(full, other)
+
+
+@pytest.mark.parametrize("K,etha", [(3, 1.0), (7, 0.8), (70, 1.1)])
+def test_bce_multi_matches_torch(K, etha):
+    """The fused device BCE (LDPCDecoderLoss's list branch) equals the reference's per-term torch
+    formula: loss and the gradient of every output (K=70 exercises the >64-term grouping)."""
+    from boosted_neural_ldpc_decoder.LDPCDecoderLoss import LDPCDecoderLoss
+    from boosted_neural_ldpc_decoder.struct.LossType import LossType
+    g = torch.Generator().manual_seed(K)
+    n0, n1 = 37, 513
+    outs = [(torch.randn(n0, n1, generator=g) * 6).to(DEV).requires_grad_() for _ in range(K)]
+    y = (torch.rand(n0, n1, generator=g) < 0.3).float().to(DEV)
+    crit = LDPCDecoderLoss(loss_type=LossType.BCE, etha=etha)
+    loss = crit(outs, y, coeff_param=list(range(K)))
+    loss.backward()
+    ref_outs = [o.detach().clone().requires_grad_() for o in outs]
+    tot, norm = 0, 0
+    for k in reversed(range(K)):
+        tot = tot + etha ** k * torch.nn.functional.binary_cross_entropy_with_logits(ref_outs[k], y)
+        norm = norm + etha ** k
+    ref = 1.0 * (tot / norm).mean()
+    ref.backward()
+    np.testing.assert_allclose(loss.item(), ref.item(), rtol=2e-6)
+    for o, r in zip(outs, ref_outs):
+        np.testing.assert_allclose(o.grad.cpu().numpy(), r.grad.cpu().numpy(), rtol=1e-5,
+                                   atol=1e-6 * r.grad.abs().max().item())
