@@ -104,10 +104,12 @@ int nldpc_fast_path(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32
  *   app_prev [B][N*Z] posterior of iteration first_iter-1 (UCN with first_iter > 0), else NULL
  *   c2v      [B][E][Z] message state in/out: read at the start when cfg->c2v_in (otherwise a
  *            fresh all-zero state), holds the state after the last iteration on return
- *   v2c      [B][E][Z] scratch, or NULL when `saved` is given
+ *   v2c      [B][E][Z] scratch of the streaming path (unused, may be NULL, when nldpc_fast_path
+ *            reports 1; also NULL-able for a non-QMS training call, which streams through `saved`)
  *   saved    device buffer of nldpc_saved_bytes() bytes that receives what nldpc_backward needs
- *            (every iteration's variable-to-check messages, and for the Boosted decoders the
- *            output clamp masks), or NULL (inference); needs every entry of `outs` non-NULL
+ *            (every iteration's variable-to-check messages -- fp32, or for QMS one int8 code per
+ *            message holding Q(m) and its clip mask --, the Boosted output clamp masks, and the
+ *            cumulative-VN-weight channel values), or NULL (inference); needs every `outs` entry
  *   stream   hipStream_t */
 int nldpc_saved_bytes(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, size_t* bytes);
 int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,

@@ -237,11 +237,11 @@ def emit(S: Spec) -> str:
             for q in range(Q):
                 for k, e in mine:
                     w(f"    lds[{own(e, q, e0)}] = {ref(q, k)};")
-                    w(f"    if constexpr (SAVE) bstore(sv, vc, {4 * (e * Z + q * ZT)}, {ref(q, k)});")
+                    w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(q, k)}, a.qbit);")
             for j, e in d1:  # v2c = (0 + xin) + 0: no other edge in the column
                 for q in range(Q):
                     w(f"    {{ const float v_ = fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f); "
-                      f"lds[{own(e, q, e0)}] = v_; if constexpr (SAVE) bstore(sv, vc, {4 * (e * Z + q * ZT)}, v_); }}")
+                      f"lds[{own(e, q, e0)}] = v_; if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qbit); }}")
             w("}")
             w("template <int KIND, bool SAVE>")
             w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
@@ -413,8 +413,10 @@ def emit(S: Spec) -> str:
         w(f"        const rsrc_t nr = make_rsrc(pn ? pn + blk * {NZ} : a.xa, pn ? nlive * {4 * NZ} : 0);")
         w("        const uint8_t* nmp = (SAVE && a.symask) ? a.symask + it * a.symask_stride : nullptr;")
         w(f"        const rsrc_t nm = make_rsrc((const float*)(nmp ? nmp + blk * {NZ} : nullptr), nmp ? nlive * {NZ} : 0);")
-        w("        float* svp = SAVE ? a.sv2c + it * a.sv2c_stride : nullptr;")
-        w(f"        const rsrc_t sv = make_rsrc(svp ? svp + blk * {S.E * Z} : a.xa, svp ? nlive * {4 * S.E * Z} : 0);")
+        w("        constexpr int SB = saved_msg_bytes<KIND>();")
+        w("        const char* svp = SAVE ? a.sv2c + it * a.sv2c_stride * SB : nullptr;")
+        w(f"        const rsrc_t sv = make_rsrc((const float*)(svp ? svp + blk * {S.E * Z} * SB : nullptr), "
+          f"svp ? nlive * {S.E * Z} * SB : 0);")
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
         for ci in range(len(S.chunks)):
             w(f"        wr_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, it, sv, vc);")
@@ -644,7 +646,10 @@ def emit_bwd(S: Spec) -> str:
     w("            auto load_m = [&](int k) {  // saved v2c of edge k at variable copy (h + s) mod Z, h = u + q*ZT")
     w("                int t = u + q * ZT + sh[k];")
     w("                t -= t >= Z ? Z : 0;")
-    w("                return bload(svr, vcw + 4u * (uint32_t)t, 4 * (e0 + k) * Z);")
+    w("                if constexpr (KIND == NLDPC_QMS)")
+    w("                    return qms_decode((int8_t)bload8(svr, (vcw >> 2) + (uint32_t)t, (e0 + k) * Z));")
+    w("                else")
+    w("                    return bload(svr, vcw + 4u * (uint32_t)t, 4 * (e0 + k) * Z);")
     w("            };")
     w("            if constexpr (KIND == NLDPC_SP) {")
     w("                float m[DC], gc[DC], gm[DC], gw[DC], gu[DC], gb[DC];")
@@ -711,8 +716,9 @@ def emit_bwd(S: Spec) -> str:
         w("        const uint8_t* mp_ = a.symask ? a.symask + it * a.symask_stride : nullptr;")
         w(f"        const rsrc_t gr = {rs('gp_', 4, NZ)};")
         w(f"        const rsrc_t mr = {rs('mp_', 1, NZ)};")
-        w("        const float* sv_ = a.sv2c + it * a.sv2c_stride;")
-        w(f"        const rsrc_t svr = make_rsrc(sv_ + blk * {E * Z}, nlive * {4 * E * Z});")
+        w("        constexpr int SB = saved_msg_bytes<KIND>();")
+        w("        const char* sv_ = a.sv2c + it * a.sv2c_stride * SB;")
+        w(f"        const rsrc_t svr = make_rsrc((const float*)(sv_ + blk * {E * Z} * SB), nlive * {E * Z} * SB);")
         w("        const float* sx_ = (a.sxin && it >= 1) ? a.sxin + (it - 1) * a.sxin_stride : nullptr;")
         w(f"        const rsrc_t sxp = {rs('sx_', 4, NZ)};")
         w("        const cfloat_p wvn = a.w_vn ? (cfloat_p)(a.w_vn + (int64_t)it * N) : nullptr;")

@@ -45,7 +45,8 @@ struct VNBArgs {
 struct CNBArgs {
     DevGraph g;
     int64_t B;
-    const float* v2c;     // saved v2c_k
+    const float* v2c;     // saved v2c_k (fp32), or nullptr when v2c_code is given
+    const int8_t* v2c_code;  // saved v2c_k as QMS int8 codes (qms_code), or nullptr
     const float* gc2v;    // dL/dc2v_{k+1}
     float* gv2c;          // dL/dv2c_k out
     const float* w_cn;    // [E] or nullptr
@@ -209,7 +210,7 @@ __device__ __forceinline__ void cnb_body(const CNBArgs& a, const Geo& q, const i
             const int t = h + a.g.e_shift[beg + k];
             vv[k] = t >= Z ? t - Z : t;
             const int64_t off = (base + beg + k) * Z + vv[k];
-            m[k] = a.v2c[off];
+            m[k] = a.v2c_code ? qms_decode(a.v2c_code[off]) : a.v2c[off];
             gc[k] = a.gc2v[off];
         } else {
             vv[k] = 0;
@@ -348,6 +349,7 @@ static hipError_t reduce_launch(const float* part, int64_t rows, int64_t nb, int
 static bool fused_bwd_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T) {
     static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
     if (disabled || (cfg->flags & NLDPC_FLAG_STREAM) || g->fused < 0) return false;
+    if (cfg->kind == NLDPC_QMS && !qms_active(cfg->qbit)) return false;  // QMS saved state = int8 codes
     return !cfg->ucn && cfg->vn_prefix == 0 && T <= kFusedMaxT;
 }
 
@@ -392,7 +394,7 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
     a.w_cn = w_cn;
     a.bias = bias;
     a.w_vn = (g_w_vn && cfg->vn_cumulative) ? w_vn : nullptr;  // the chain only feeds dL/dw_vn
-    a.sv2c = reinterpret_cast<const float*>(sb + SL.v2c_off);
+    a.sv2c = sb + SL.v2c_off;
     a.symask = SL.has_ymask ? reinterpret_cast<const uint8_t*>(sb + SL.ymask_off) : nullptr;
     a.sxin = SL.has_xin ? reinterpret_cast<const float*>(sb + SL.xin_off) : nullptr;
     a.sv2c_stride = SL.v2c_stride;
@@ -453,7 +455,7 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
     if (fusedb) return fused_backward(g, cfg, B, T, xa, w_cn, bias, w_vn, grad_outs, saved, g_w_cn, g_bias, g_w_vn, work, s);
     const DevGraph& G = g->dev;
     const SavedLayout SL = saved_layout(g, cfg, B, T);
-    const float* sv2c = reinterpret_cast<const float*>(static_cast<const char*>(saved) + SL.v2c_off);
+    const char* sv2c = static_cast<const char*>(saved) + SL.v2c_off;  // fp32, or QMS int8 codes
     const uint8_t* smask = SL.has_ymask ? static_cast<const uint8_t*>(saved) + SL.ymask_off : nullptr;
     const float* sxin = SL.has_xin ? reinterpret_cast<const float*>(static_cast<const char*>(saved) + SL.xin_off) : nullptr;
     char* wb = static_cast<char*>(work);
@@ -483,7 +485,8 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
         if (cfg->ucn) app = k >= 1 ? outs[k - 1] : (cfg->first_iter > 0 ? app_prev : nullptr);
         CNBArgs ca{G,
                    B,
-                   sv2c + (int64_t)k * SL.v2c_stride,
+                   SL.v2c_code ? nullptr : reinterpret_cast<const float*>(sv2c) + (int64_t)k * SL.v2c_stride,
+                   SL.v2c_code ? reinterpret_cast<const int8_t*>(sv2c) + (int64_t)k * SL.v2c_stride : nullptr,
                    gc,
                    gv,
                    w_cn ? w_cn + (int64_t)k * G.E : nullptr,

@@ -25,6 +25,7 @@ struct VNArgs {
     const float* xa;     // [B][N][Z]
     const float* c2v;    // [B][E][Z] or nullptr (all-zero state)
     float* v2c;          // [B][E][Z] or nullptr (posterior only)
+    int8_t* v2c_code;    // [B][E][Z] QMS int8 codes of v2c (saved for the backward), or nullptr
     float* post;         // [B][N][Z] or nullptr
     uint8_t* ymask;      // [B][N][Z] clamp mask of the posterior (training) or nullptr
     const float* w_vn;   // [steps][N] cumulative VN weights (boosted) or nullptr
@@ -105,7 +106,9 @@ __device__ __forceinline__ void vn_body(const VNArgs& a, const Geo& q, const int
 #pragma unroll
                 for (int m = k + 1; m < DV; ++m)
                     if (m < d) S = fadd(S, c[m]);
-                a.v2c[(base + eidx[k]) * Z + v] = fadd(x0, S);
+                const float m = fadd(x0, S);
+                a.v2c[(base + eidx[k]) * Z + v] = m;
+                if (KIND == NLDPC_QMS && a.v2c_code) a.v2c_code[(base + eidx[k]) * Z + v] = (int8_t)qms_code(m, a.qbit);
                 P = fadd(P, c[k]);
             }
         }
@@ -233,8 +236,9 @@ SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     SavedLayout L;
     const int64_t EZ = (int64_t)g->dev.E * g->dev.Z, NZ = (int64_t)g->dev.N * g->dev.Z;
     L.v2c_off = 0;
-    L.v2c_stride = B * EZ;  // floats per iteration
-    const size_t v2c_bytes = (size_t)T * B * EZ * sizeof(float);
+    L.v2c_stride = B * EZ;  // messages per iteration
+    L.v2c_code = cfg->kind == NLDPC_QMS && qms_active(cfg->qbit);
+    const size_t v2c_bytes = (size_t)T * B * EZ * (L.v2c_code ? 1 : sizeof(float));
     L.ymask_off = (v2c_bytes + 255) & ~(size_t)255;
     L.ymask_stride = B * NZ;  // bytes per iteration
     L.has_ymask = cfg->kind != NLDPC_NEURAL;
@@ -249,7 +253,8 @@ SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
 static bool fused_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T, bool saving) {
     static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
     if (disabled || (cfg->flags & NLDPC_FLAG_STREAM)) return false;
-    (void)saving;  // the SAVE kernels write what the backward needs
+    // the SAVE kernels write what the backward needs (QMS: int8 codes, which need an active quantiser)
+    if (saving && cfg->kind == NLDPC_QMS && !qms_active(cfg->qbit)) return false;
     return g->fused >= 0 && !cfg->ucn && !cfg->c2v_in && T <= kFusedMaxT;
 }
 
@@ -274,7 +279,7 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     if (saved) {
         const SavedLayout SL = saved_layout(g, cfg, B, T);
         char* sb = static_cast<char*>(saved);
-        fa.sv2c = reinterpret_cast<float*>(sb + SL.v2c_off);
+        fa.sv2c = sb + SL.v2c_off;  // QMS: int8 codes (the kernel knows from its kind)
         fa.sv2c_stride = SL.v2c_stride;
         fa.symask = SL.has_ymask ? reinterpret_cast<uint8_t*>(sb + SL.ymask_off) : nullptr;
         fa.symask_stride = SL.ymask_stride;
@@ -346,7 +351,9 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
     if (!v2c && !saved) return fail(NLDPC_EINVAL, "nldpc_forward: need v2c scratch or saved buffer");
     const DevGraph& G = g->dev;
     const SavedLayout SL = saved_layout(g, cfg, B, T);
-    float* saved_v2c = saved ? reinterpret_cast<float*>(static_cast<char*>(saved) + SL.v2c_off) : nullptr;
+    float* saved_v2c = (saved && !SL.v2c_code) ? reinterpret_cast<float*>(static_cast<char*>(saved) + SL.v2c_off) : nullptr;
+    int8_t* saved_code = (saved && SL.v2c_code) ? reinterpret_cast<int8_t*>(static_cast<char*>(saved) + SL.v2c_off) : nullptr;
+    if (saved_code && !v2c) return fail(NLDPC_EINVAL, "nldpc_forward: QMS training needs the v2c scratch");
     uint8_t* saved_mask = (saved && SL.has_ymask) ? static_cast<uint8_t*>(saved) + SL.ymask_off : nullptr;
     float* saved_xin = (saved && SL.has_xin) ? reinterpret_cast<float*>(static_cast<char*>(saved) + SL.xin_off) : nullptr;
     bool state_valid = cfg->c2v_in != 0;
@@ -357,6 +364,7 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
                   xa,
                   state_valid ? c2v : nullptr,
                   v2c_k,
+                  saved_code ? saved_code + (int64_t)k * SL.v2c_stride : nullptr,
                   k >= 1 ? outs[k - 1] : nullptr,
                   (k >= 1 && saved_mask) ? saved_mask + (int64_t)(k - 1) * SL.ymask_stride : nullptr,
                   cfg->vn_cumulative ? w_vn : nullptr,
@@ -392,7 +400,7 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
         state_valid = true;
     }
     if (outs[T - 1]) {
-        VNArgs va{G, B, xa, c2v, nullptr, outs[T - 1],
+        VNArgs va{G, B, xa, c2v, nullptr, nullptr, outs[T - 1],
                   saved_mask ? saved_mask + (int64_t)(T - 1) * SL.ymask_stride : nullptr, nullptr, 0, nullptr,
                   nullptr, cfg->qbit,
                   cfg->llr_lo, cfg->llr_hi};

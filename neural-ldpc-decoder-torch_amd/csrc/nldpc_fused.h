@@ -24,7 +24,7 @@ struct FusedArgs {
     float lo, hi;
     float* c2v_out;      // [B][E][Z] final message state, or nullptr
     // what the backward needs (SAVE kernels only; SavedLayout in nldpc_internal.h)
-    float* sv2c;         // [T][B][E][Z] v2c of every iteration
+    char* sv2c;          // [T][B][E][Z] v2c of every iteration (fp32; QMS: int8 codes, qms_code)
     uint8_t* symask;     // [T][B][N][Z] posterior clamp masks (Boosted), or nullptr
     float* sxin;         // [T][B][N][Z] channel value xin of every iteration (cumulative VN weights), or nullptr
     int64_t sv2c_stride, symask_stride, sxin_stride;  // elements per iteration
@@ -50,6 +50,12 @@ __device__ __forceinline__ void bstore(rsrc_t r, uint32_t vo, int so, float v) {
 __device__ __forceinline__ void bstore8(rsrc_t r, uint32_t vo, int so, bool v) {
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, vo, so, 0);
 }
+__device__ __forceinline__ void bstore_i8(rsrc_t r, uint32_t vo, int so, int v) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v & 0xff), r, vo, so, 0);
+}
+// bytes per saved v2c message of a kernel kind (QMS saves int8 codes)
+template <int KIND>
+constexpr int saved_msg_bytes() { return KIND == NLDPC_QMS ? 1 : 4; }
 
 // Channel value the VN adds.  With cumulative VN weights (Boosted, w_vn set) the registers hold xin
 // itself, advanced one step per iteration by chan_step (Boosted…py:325-337: xin <- Q(xin * w_t)),
@@ -81,6 +87,13 @@ template <int KIND>
 __device__ __forceinline__ f2 posterior2(f2 xav, f2 P, const FusedArgs& a) {
     if (KIND == NLDPC_NEURAL) return xav + P;
     return f2{posterior<KIND>(xav.x, P.x, a), posterior<KIND>(xav.y, P.y, a)};
+}
+
+// one saved v2c message (training forward): fp32, or the QMS int8 code (byte offset = float offset / 4)
+template <int KIND>
+__device__ __forceinline__ void save_v2c(rsrc_t r, uint32_t vc, int elem, float v, int qbit) {
+    if constexpr (KIND == NLDPC_QMS) bstore_i8(r, vc >> 2, elem, qms_code(v, qbit));
+    else bstore(r, vc, 4 * elem, v);
 }
 
 // Boosted posterior and its clamp mask (saved for the backward): in_range of the pre-clamp value
@@ -150,7 +163,7 @@ struct FusedBwdArgs {
     const float* w_cn;     // [T][E] or nullptr
     const float* bias;     // [T][E] (Neural) or nullptr
     const float* w_vn;     // [T][N] or nullptr
-    const float* sv2c;     // saved [T][B][E][Z]
+    const char* sv2c;      // saved [T][B][E][Z] (fp32; QMS: int8 codes)
     const uint8_t* symask; // saved [T][B][N][Z] or nullptr (Neural)
     const float* sxin;     // saved [T][B][N][Z] or nullptr
     int64_t sv2c_stride, symask_stride, sxin_stride;

@@ -62,11 +62,13 @@ struct DeviceGuard {
 //   ymask [T][B][N][Z] uint8 clamp mask of every posterior (Boosted decoders only)
 //   xin   [T][B][N][Z] fp32 channel value xin_k each iteration used (cumulative VN weighting only),
 //         so neither direction re-runs the Q(x*w) chain from xa (O(T^2) over an unrolled forward)
+//   (QMS with an active quantiser saves v2c as int8 codes instead, nldpc_math.h qms_code)
 struct SavedLayout {
     size_t v2c_off, ymask_off, xin_off, total;
-    int64_t v2c_stride, ymask_stride, xin_stride;
-    bool has_ymask, has_xin;
+    int64_t v2c_stride, ymask_stride, xin_stride;  // elements per iteration
+    bool has_ymask, has_xin, v2c_code;
 };
+inline bool qms_active(int q) { return q == 6 || q == 5 || q == -5 || q == 4 || q == 3; }
 SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T);
 int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T);
 

@@ -58,6 +58,18 @@ __device__ __forceinline__ float quantize(float x, int q) {
     return active ? r : x;
 }
 
+// QMS training state.  The backward reads a saved v2c message m only through Q(m) and the STE mask of
+// Q's clip on m, so QMS saves one signed byte 2*m' per message: m' = Q(m) inside the clip range and
+// sign(m) * (hi + 1) outside it, which gives Q(m') == Q(m) and the same mask (Q's values are
+// multiples of 1/2 with |2 m'| <= 33).  A quarter of the fp32 traffic, both directions.
+__device__ __forceinline__ int qms_code(float m, int q) {
+    const QRange r = q_range(q);
+    const float qv = quantize(m, q);
+    const float mp = (m >= r.lo && m <= r.hi) ? qv : (m > 0.f ? r.hi + 1.f : -(r.hi + 1.f));
+    return (int)rintf(2.f * mp);
+}
+__device__ __forceinline__ float qms_decode(int c) { return 0.5f * (float)c; }
+
 // STE / clamp gradient mask: 1 on the closed interval (torch.clamp backward), else 0
 __device__ __forceinline__ float in_range(float x, float lo, float hi) { return (x >= lo && x <= hi) ? 1.f : 0.f; }
 

@@ -83,7 +83,8 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
         nbytes = ctypes.c_size_t(0)
         _lib.check(L.nldpc_saved_bytes(h, ctypes.byref(c), B, T, ctypes.byref(nbytes)), "nldpc_saved_bytes")
         saved = torch.empty((int(nbytes.value),), dtype=torch.uint8, device=dev)
-    scratch = None if (save or fast.value) else torch.empty((B, E, Z), dtype=torch.float32, device=dev)
+    # the streaming path works on a v2c scratch (training too: QMS saves int8 codes, not the messages)
+    scratch = None if fast.value else torch.empty((B, E, Z), dtype=torch.float32, device=dev)
     tensors = [None if (out_mask is not None and not out_mask[t]) else outs[t] for t in range(T)]
     pp, keep = _lib.ptr_array(tensors)
     w_cn, w_ucn, bias, w_vn = _f32c(w_cn), _f32c(w_ucn), _f32c(bias), _f32c(w_vn)

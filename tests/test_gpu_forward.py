@@ -180,7 +180,7 @@ def test_saved_activations_fused_equal_stream(kind, prefix, Z, B):
     assert torch.equal(res["stream"][1], res["fused"][1])
     # sections of the saved buffer (SavedLayout, nldpc_internal.h); the alignment gaps are not written
     al = lambda n: (n + 255) // 256 * 256  # noqa: E731
-    v2c = T * B * g.E * Z * 4
+    v2c = T * B * g.E * Z * (1 if kind == 2 else 4)  # QMS saves int8 codes (qms_code)
     secs = [(0, v2c)]
     end = v2c
     if kind != KIND_NEURAL:
