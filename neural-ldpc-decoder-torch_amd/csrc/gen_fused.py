@@ -26,6 +26,9 @@ import numpy as np
 
 PARTS = [int(x) for x in filter(None, os.environ.get("NLDPC_GEN_PARTS", "").split(","))]  # debug
 SKIP = set(filter(None, os.environ.get("NLDPC_GEN_SKIP", "").split(",")))  # debug: drop phases
+# diagnostic build only (make STAMPS=1 -> lib_stamps/): s_memtime at every phase boundary of the forward
+# kernels, lane 0 of each wave, first 256 workgroups (FusedArgs::stamps, tools/stamps.py)
+STAMPS = os.environ.get("NLDPC_GEN_STAMPS") == "1"
 LDS_BYTES = 160 * 1024 - 2048  # leave room for the compiler / alignment
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q)
@@ -146,32 +149,49 @@ def emit(S: Spec) -> str:
     def X(j, q):  # byte offset of variable copy (column j, lane copy q) in a [N][Z] codeword
         return 4 * (j * Z + q * ZT)
 
-    def vn_group(p, n, j, s, d, final, vec, names, xin):
-        """VN (or final posterior) of column j (n-th register column of part p) for one copy group:
-        vec: float2 pair (names = ('cp0', 'x'/'y' copies)) or scalar."""
-        T_ = "f2" if vec else "float"
-        arr = names
-        c = lambda k: f"{arr}[{s + k}]"  # noqa: E731
-        add = (lambda x, y: f"({x} + {y})") if vec else (lambda x, y: f"fadd({x}, {y})")  # noqa: E731
-        zero = "f2{0.f, 0.f}" if vec else "0.f"
-        w(f"        {{  // column {j}, degree {d}, {'copies ' + xin if vec else 'copy ' + xin}")
-        w(f"            {T_} P = {zero};")
+    def vn_col(p, n, j, s, d, final):
+        """VN (or final posterior) of column j (n-th register column of part p) for every copy group of
+        the lane at once: the packed-pair chains (v_pk_add_f32, copies 2i/2i+1) and the scalar chain
+        (last copy) are emitted interleaved, so consecutive adds never depend on each other (gfx950
+        puts an s_nop between two dependent packed adds).  Each chain is the reference's sequential
+        fp32 order: S_k = ((P_{k-1} + c_{k+1}) + ...) + c_{d-1}, v2c_k = x0 + S_k, P_k = P_{k-1} + c_k."""
+        grp = [("f2", f"cp{i}", f"xp{i}[{n}]", str(i)) for i in range(NPAIR)]
+        if SINGLE:
+            grp.append(("float", "cs", f"xs[{n}]", "s"))
+
+        def add(T_, x, y):
+            return f"({x} + {y})" if T_ == "f2" else f"fadd({x}, {y})"
+
+        def zero(T_):
+            return "f2{0.f, 0.f}" if T_ == "f2" else "0.f"
+
+        w(f"        {{  // column {j}, degree {d}")
+        for T_, arr, xin, g in grp:
+            w(f"            {T_} P_{g} = {zero(T_)};")
         if not final:
-            ch = f"chan2<KIND>({xin}, a)" if vec else f"chan<KIND>({xin}, a)"
-            w(f"            const {T_} x0 = {add(zero, ch)};")
+            for T_, arr, xin, g in grp:
+                ch = f"chan2<KIND>({xin}, a)" if T_ == "f2" else f"chan<KIND>({xin}, a)"
+                w(f"            const {T_} x0_{g} = {add(T_, zero(T_), ch)};")
             for k in range(d):
-                expr = "P"
+                w("            {")
+                for T_, arr, xin, g in grp:
+                    w(f"                {T_} S_{g} = P_{g};")
                 for m in range(k + 1, d):
-                    expr = add(expr, c(m))
-                # one edge at a time: the fake dependence of the running prefix on the new message
-                # keeps the compiler from running the prefix chain ahead and holding every partial
-                # sum in a register (dependent VALU ops issue back to back anyway)
-                w(f"            {{ const {T_} S_ = {expr}; const {T_} o_ = {c(k)}; {c(k)} = {add('x0', 'S_')}; "
-                  f"asm volatile(\"\" : \"+v\"(P) : \"v\"({c(k)})); P = {add('P', 'o_')}; }}")
+                    for T_, arr, xin, g in grp:
+                        w(f"                S_{g} = {add(T_, f'S_{g}', f'{arr}[{s + m}]')};")
+                for T_, arr, xin, g in grp:
+                    w(f"                const {T_} o_{g} = {arr}[{s + k}]; {arr}[{s + k}] = {add(T_, f'x0_{g}', f'S_{g}')};")
+                # the fake dependence of the running prefix on the new message keeps the compiler from
+                # running the prefix chain ahead and holding every partial sum in a register
+                for T_, arr, xin, g in grp:
+                    w(f"                asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]));")
+                for T_, arr, xin, g in grp:
+                    w(f"                P_{g} = {add(T_, f'P_{g}', f'o_{g}')};")
+                w("            }")
         else:
             for k in range(d):
-                w(f"            P = {add('P', c(k))};")
-        return T_
+                for T_, arr, xin, g in grp:
+                    w(f"            P_{g} = {add(T_, f'P_{g}', f'{arr}[{s + k}]')};")
 
     for p in range(S.P):
         cols = S.reg_cols[p]
@@ -183,35 +203,36 @@ def emit(S: Spec) -> str:
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
+                vn_col(p, n, j, s, d, final)
                 for i in range(NPAIR):
-                    vn_group(p, n, j, s, d, final, True, f"cp{i}", f"xp{i}[{n}]")
+                    w("            {")
                     w(f"            const f2 xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? f2{{bload(xr, vo, {X(j, 2 * i)}), "
                       f"bload(xr, vo, {X(j, 2 * i + 1)})}} : xp{i}[{n}];")
                     w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w("                bool m0_, m1_;")
-                    w(f"                bstore(pr, vo, {X(j, 2 * i)}, posterior_m<KIND>(xo_.x, P.x, a, m0_));")
-                    w(f"                bstore(pr, vo, {X(j, 2 * i + 1)}, posterior_m<KIND>(xo_.y, P.y, a, m1_));")
+                    w(f"                bstore(pr, vo, {X(j, 2 * i)}, posterior_m<KIND>(xo_.x, P_{i}.x, a, m0_));")
+                    w(f"                bstore(pr, vo, {X(j, 2 * i + 1)}, posterior_m<KIND>(xo_.y, P_{i}.y, a, m1_));")
                     w(f"                bstore8(pm, vm, {X(j, 2 * i) // 4}, m0_);")
                     w(f"                bstore8(pm, vm, {X(j, 2 * i + 1) // 4}, m1_);")
                     w("            } else {")
-                    w("                const f2 y_ = posterior2<KIND>(xo_, P, a);")
+                    w(f"                const f2 y_ = posterior2<KIND>(xo_, P_{i}, a);")
                     w(f"                bstore(pr, vo, {X(j, 2 * i)}, y_.x);")
                     w(f"                bstore(pr, vo, {X(j, 2 * i + 1)}, y_.y);")
                     w("            }")
-                    w("        }")
-                    w("        __builtin_amdgcn_sched_barrier(0);")
+                    w("            }")
                 if SINGLE:
-                    vn_group(p, n, j, s, d, final, False, "cs", f"xs[{n}]")
+                    w("            {")
                     w(f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, Q - 1)}) : xs[{n}];")
                     w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w("                bool m_;")
-                    w(f"                bstore(pr, vo, {X(j, Q - 1)}, posterior_m<KIND>(xo_, P, a, m_));")
+                    w(f"                bstore(pr, vo, {X(j, Q - 1)}, posterior_m<KIND>(xo_, P_s, a, m_));")
                     w(f"                bstore8(pm, vm, {X(j, Q - 1) // 4}, m_);")
                     w("            } else {")
-                    w(f"                bstore(pr, vo, {X(j, Q - 1)}, posterior<KIND>(xo_, P, a));")
+                    w(f"                bstore(pr, vo, {X(j, Q - 1)}, posterior<KIND>(xo_, P_s, a));")
                     w("            }")
-                    w("        }")
-                    w("        __builtin_amdgcn_sched_barrier(0);")
+                    w("            }")
+                w("        }")
+                w("        __builtin_amdgcn_sched_barrier(0);")
                 s += d
             w("}")
 
@@ -310,8 +331,11 @@ def emit(S: Spec) -> str:
     w("#pragma unroll")
     w(f"        for (int q = 0; q < {Q}; ++q) {{  // one check copy at a time: the state owns the registers")
     w("            float m[DC];")
+    w("            int ro = (e0 - e0c) * Z + u + q * ZT;  // one base VGPR per row copy: the edges ride in the")
+    w("            asm volatile(\"\" : \"+v\"(ro));  // 16-bit DS offset (no per-edge address add)")
+    w("            float* rq = lds + ro;")
     w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) m[k] = rp[k * Z + q * ZT];")
+    w("            for (int k = 0; k < DC; ++k) m[k] = rq[k * Z];")
     w("            if (KIND == NLDPC_NEURAL) {")
     w("                neural_row<DC>(m, wv, bv);")
     w("            } else {")
@@ -323,7 +347,7 @@ def emit(S: Spec) -> str:
       " a.lo, a.hi).c;")
     w("            }")
     w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) rp[k * Z + q * ZT] = m[k];")
+    w("            for (int k = 0; k < DC; ++k) rq[k * Z] = m[k];")
     if Q > 1:
         w("            __builtin_amdgcn_sched_barrier(0);")
     w("        }")
@@ -389,7 +413,13 @@ def emit(S: Spec) -> str:
         w("        for (int s_ = 0; s_ < a.vn_prefix; ++s_)")
         chan_steps("s_", "            ")
         w("    }")
+        def stamp(ph):
+            if STAMPS and len(S.chunks) == 2:
+                w(f"        if (a.stamps && blockIdx.x < 256 && (threadIdx.x & 63) == 0) "
+                  f"a.stamps[((blockIdx.x * {S.threads // 64} + (threadIdx.x >> 6)) * a.T + it) * 8 + {ph}] = "
+                  f"__builtin_amdgcn_s_memtime();")
         w("    for (int it = 0; it < a.T; ++it) {")
+        stamp(0)
         w("        if (KIND != NLDPC_NEURAL && a.w_vn) {")
         chan_steps("a.vn_prefix + it", "            ")
         w("            if constexpr (SAVE) {")
@@ -418,14 +448,18 @@ def emit(S: Spec) -> str:
         w(f"        const rsrc_t sv = make_rsrc((const float*)(svp ? svp + blk * {S.E * Z} * SB : nullptr), "
           f"svp ? nlive * {S.E * Z} * SB : 0);")
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
+        stamp(1)
         for ci in range(len(S.chunks)):
             w(f"        wr_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, it, sv, vc);")
+            stamp(2 + 3 * ci)
             w("        __syncthreads();")
             if "cn" not in SKIP:
                 for dc, t0, n in S.cn_groups[(p, ci)]:
                     w(f"        cn_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]});")
+            stamp(3 + 3 * ci)
             w("        __syncthreads();")
             w(f"        rd_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm);")
+            stamp(4 + 3 * ci)
             w("        __syncthreads();")
         w("    }")
         w("    const float* pl = a.outs.p[a.T - 1];")

@@ -13,7 +13,9 @@
 // Message state is [B][E][Z] fp32 in HBM with E in C-order; see DESIGN.md for the roofline.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "nldpc_fused.h"
 
@@ -286,6 +288,11 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
         fa.sxin = SL.has_xin ? reinterpret_cast<float*>(sb + SL.xin_off) : nullptr;
         fa.sxin_stride = SL.xin_stride;
     }
+    // diagnostic stamp build (lib_stamps/): NLDPC_STAMPS=<file> collects the phase stamps of each call
+    static const char* stamp_file = std::getenv("NLDPC_STAMPS");
+    const size_t stamp_n = (size_t)256 * (f.threads / 64) * T * 8;
+    if (stamp_file) NLDPC_HIP_CHECK(hipMalloc(&fa.stamps, stamp_n * sizeof(uint64_t)));
+    if (stamp_file) NLDPC_HIP_CHECK(hipMemsetAsync(fa.stamps, 0, stamp_n * sizeof(uint64_t), s));
     void* args[] = {&fa};
     const int64_t blocks = (B + f.G - 1) / f.G;
     prof_start(PROF_FUSED, s);
@@ -293,6 +300,18 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
                                    0, s);
     prof_stop(s);
     if (e == hipSuccess) e = hipGetLastError();
+    if (stamp_file && e == hipSuccess) {
+        std::vector<uint64_t> h(stamp_n);
+        NLDPC_HIP_CHECK(hipStreamSynchronize(s));
+        NLDPC_HIP_CHECK(hipMemcpy(h.data(), fa.stamps, stamp_n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        if (FILE* fp = std::fopen(stamp_file, "wb")) {
+            const int32_t hdr[4] = {256, f.threads / 64, T, 8};
+            std::fwrite(hdr, sizeof(hdr), 1, fp);
+            std::fwrite(h.data(), sizeof(uint64_t), stamp_n, fp);
+            std::fclose(fp);
+        }
+        (void)hipFree(fa.stamps);
+    }
     return e == hipSuccess ? NLDPC_OK : hip_fail(e, "fused kernel launch");
 }
 

@@ -29,6 +29,7 @@ struct FusedArgs {
     float* sxin;         // [T][B][N][Z] channel value xin of every iteration (cumulative VN weights), or nullptr
     int64_t sv2c_stride, symask_stride, sxin_stride;  // elements per iteration
     OutPtrs outs;        // T posteriors [B][N][Z] (nullptr entries are skipped)
+    uint64_t* stamps;    // diagnostic stamp build only (make STAMPS=1): [256][waves][T][8] s_memtime
 };
 
 // Global memory of the fused kernels goes through buffer descriptors built from wave-uniform values:

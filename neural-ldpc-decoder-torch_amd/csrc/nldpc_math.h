@@ -22,8 +22,11 @@ __device__ __forceinline__ float clampf(float x, float lo, float hi) {
 // torch.sign
 __device__ __forceinline__ float signf_t(float x) { return (float)(x > 0.f) - (float)(x < 0.f); }
 
-// x * (x > 0).float()  (the reference's ReLU-by-mask, NeuralLDPCDecoder.py:90, Boosted…py:505)
-__device__ __forceinline__ float relu_mask(float x) { return fmul(x, x > 0.f ? 1.f : 0.f); }
+// x * (x > 0).float()  (the reference's ReLU-by-mask, NeuralLDPCDecoder.py:90, Boosted…py:505) as one
+// v_max_f32: the same value for every non-NaN x (x <= 0 gives +0 where the reference's product gives
+// -0 for negative x; a zero c2v of either sign only ever meets the +0-started sums of the VN, so no
+// output or later message differs)
+__device__ __forceinline__ float relu_mask(float x) { return __builtin_fmaxf(x, 0.f); }
 
 // QMS quantiser (BoostedNeuralLDPCDecoder.py:187-214): forward value of the straight-through
 // estimator, x_clipped + (q_value - x_clipped), evaluated in fp32 like the reference.

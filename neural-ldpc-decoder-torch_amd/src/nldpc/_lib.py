@@ -16,7 +16,7 @@ import threading
 import torch  # noqa: F401  (must be loaded first, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libnldpc.so"))
+LIB_PATH = os.environ.get("NLDPC_LIB_PATH") or os.path.normpath(os.path.join(_HERE, "..", "..", "lib", "libnldpc.so"))
 
 NLDPC_OK, NLDPC_EINVAL, NLDPC_EHIP, NLDPC_EUNSUPPORTED = 0, 1, 2, 3
 NLDPC_SP, NLDPC_MS, NLDPC_QMS, NLDPC_NEURAL = 0, 1, 2, 3
