@@ -90,6 +90,7 @@ class Spec:
         self.threads = P * self.lanes
         assert self.threads <= 1024 and self.lanes % 64 == 0, (tag, self.threads)
         self.max_dc = max(len(r) for r in self.row_edges)
+        self.hb_cols = cols  # column of each C-order edge
 
 
 def emit(S: Spec) -> str:
@@ -102,6 +103,8 @@ def emit(S: Spec) -> str:
       f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B")
     w(f"namespace fused_{S.tag} {{")
     w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E};")
+    w("// degree-1 edges bypass LDS (Neural inference; see the check-node section)")
+    w("#define D1_BYPASS (KIND == NLDPC_NEURAL && !SAVE)")
 
     # Register state of part p: copies are paired (q = 0,1 / 2,3 ...) into float2 arrays so the VN's
     # additions run as packed fp32 (v_pk_add_f32: two IEEE adds per lane, same rounding); an odd
@@ -259,10 +262,14 @@ def emit(S: Spec) -> str:
                 for k, e in mine:
                     w(f"    lds[{own(e, q, e0)}] = {ref(q, k)};")
                     w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(q, k)}, a.qbit);")
-            for j, e in d1:  # v2c = (0 + xin) + 0: no other edge in the column
+            if d1:  # v2c = (0 + xin) + 0: no other edge in the column (bypass: the check node reads xa)
+                w("    if constexpr (!D1_BYPASS) {")
+            for j, e in d1:
                 for q in range(Q):
                     w(f"    {{ const float v_ = fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f); "
                       f"lds[{own(e, q, e0)}] = v_; if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qbit); }}")
+            if d1:
+                w("    }")
             w("}")
             w("template <int KIND, bool SAVE>")
             w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
@@ -272,7 +279,9 @@ def emit(S: Spec) -> str:
             for q in range(Q):
                 for k, e in mine:
                     w(f"    {ref(q, k)} = lds[{own(e, q, e0)}];")
-            for j, e in d1:  # this iteration's posterior right away
+            if d1:  # this iteration's posterior right away (bypass: written by the check node)
+                w("    if constexpr (!D1_BYPASS) {")
+            for j, e in d1:
                 for q in range(Q):
                     w(f"    {{ const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
                     w(f"      const float P_ = fadd(0.f, lds[{own(e, q, e0)}]);")
@@ -286,73 +295,84 @@ def emit(S: Spec) -> str:
                     for q in range(Q):
                         w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, lds[{own(e, q, e0)}]);")
                 w("    }")
+                w("    }")
             w("}")
 
-    # ---------------------------------------------------------------- check nodes (table driven)
+    # ---------------------------------------------------------------- check nodes
     # LDS holds each edge's Z messages in CHECK order (the owners rotate on write/read-back), so the
-    # thread of check copy h reads every edge of its row at h: one address per row, the edges at
-    # immediate offsets k*Z.  Rows are grouped by degree so every loop has a compile-time degree.
-    tab, groups = [], {}
+    # thread of check copy h reads every edge of its row at h: one address per row copy, the edges at
+    # immediate offsets k*Z.  Rows are emitted inline per part and chunk (literal edges and degree).
+    # D1_BYPASS (Neural inference): a degree-1 edge's v2c is the channel value itself, so instead of a
+    # round trip owner -> LDS -> check node -> LDS -> owner, the check-node thread keeps that edge's xa
+    # (at its rotated copies) in registers from the start and writes the edge's posterior (and final
+    # c2v) itself: ~19% of the LDS traffic of BG2 (38 of 197 edges) disappears.
+    d1set = {S.col_edges[j][0] for j in range(S.N) if len(S.col_edges[j]) == 1}
+    S.cd_index = {}  # part -> list of (edge, q) whose xa the check-node thread holds
     for p in range(S.P):
-        for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
-            gl = []
-            rows = S.cn_rows[ci][p]
-            for dc in sorted({len(S.row_edges[i]) for i in rows}, reverse=True):
-                sel = [i for i in rows if len(S.row_edges[i]) == dc]
-                gl.append((dc, len(tab), len(sel)))
-                tab += [S.row_edges[i][0] for i in sel]
-            groups[(p, ci)] = gl
-    S.cn_groups = groups
-    w(f"static __constant__ int32_t cn_tab[{max(1, len(tab))}] = {{{', '.join(str(x) for x in tab) or '0'}}};")
-    w("template <int KIND, int DC>")
-    w("__device__ __forceinline__ void cn_rows(float* lds, int u, const FusedArgs& a, int it, int t0, int n, int e0c) {")
-    w("    asm volatile(\"\" : \"+v\"(u));")
-    w("    for (int r = 0; r < n; ++r) {")
-    w("        const int e0 = cn_tab[t0 + r];  // first edge of the row (its edges are consecutive)")
-    w("        float* rp = lds + (e0 - e0c) * Z + u;")
-    w("        float wv[DC], bv[DC];")
-    w("        const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + e0) : nullptr;")
-    w("        const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + e0) : nullptr;")
-    w("        // whole-row scalar loads (one uniform test per row, not per edge, so the loads can merge)")
-    w("        if (KIND == NLDPC_NEURAL || wc) {")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) wv[k] = wc[k];")
-    w("        } else {")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) wv[k] = 1.f;")
-    w("        }")
-    w("        if (KIND == NLDPC_NEURAL || bs) {")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) bv[k] = bs[k];")
-    w("        } else {")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) bv[k] = 0.f;")
-    w("        }")
-    w("#pragma unroll")
-    w(f"        for (int q = 0; q < {Q}; ++q) {{  // one check copy at a time: the state owns the registers")
-    w("            float m[DC];")
-    w("            int ro = (e0 - e0c) * Z + u + q * ZT;  // one base VGPR per row copy: the edges ride in the")
-    w("            asm volatile(\"\" : \"+v\"(ro));  // 16-bit DS offset (no per-edge address add)")
-    w("            float* rq = lds + ro;")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) m[k] = rq[k * Z];")
-    w("            if (KIND == NLDPC_NEURAL) {")
-    w("                neural_row<DC>(m, wv, bv);")
-    w("            } else {")
-    w("                CnCore<DC> core;")
-    w("                cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core);")
-    w("#pragma unroll")
-    w("                for (int k = 0; k < DC; ++k)")
-    w("                    m[k] = cn_epilogue<KIND, false>(core.out0[k], wv[k], 0.f, 0.f, 0.f, wc != nullptr, false, a.qbit,"
-      " a.lo, a.hi).c;")
-    w("            }")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) rq[k * Z] = m[k];")
-    if Q > 1:
-        w("            __builtin_amdgcn_sched_barrier(0);")
-    w("        }")
-    w("    }")
-    w("}")
+        lst = []
+        for ci in range(len(S.chunks)):
+            for i in S.cn_rows[ci][p]:
+                for e in S.row_edges[i]:
+                    if e in d1set:
+                        for q in range(Q):
+                            lst.append((e, q))
+        S.cd_index[p] = lst
+
+    def rot(e, q):  # check copy h = u + q*ZT of edge e sits at variable copy (u + c) mod Z
+        c = (q * ZT + int(S.shift[e])) % Z
+        dv = f"(u >= {Z - c} ? {(-4 * Z) & 0xFFFFFFFF}u : 0u)" if c + ZT > Z else "0u"
+        return c, dv
+
+    for p in range(S.P):
+        ncd = max(len(S.cd_index[p]), 1)
+        for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
+            w("template <int KIND, bool SAVE>")
+            w(f"__device__ __forceinline__ void cn_p{p}_c{ci}(float* lds, int u, const FusedArgs& a, int it, "
+              f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last) {{")
+            w("    asm volatile(\"\" : \"+v\"(u));")
+            rows = sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i]))
+            for i in rows:
+                es = S.row_edges[i]
+                DC, e0 = len(es), es[0]
+                w(f"    {{  // check row {i}: edges {e0}..{e0 + DC - 1}")
+                w(f"        float wv[{DC}], bv[{DC}];")
+                w(f"        const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + {e0}) : nullptr;")
+                w(f"        const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + {e0}) : nullptr;")
+                w("        // whole-row scalar loads (one uniform test per row, not per edge, so the loads can merge)")
+                w(f"        if (KIND == NLDPC_NEURAL || wc) {{ for (int k = 0; k < {DC}; ++k) wv[k] = wc[k]; }}")
+                w(f"        else {{ for (int k = 0; k < {DC}; ++k) wv[k] = 1.f; }}")
+                w(f"        if (KIND == NLDPC_NEURAL || bs) {{ for (int k = 0; k < {DC}; ++k) bv[k] = bs[k]; }}")
+                w(f"        else {{ for (int k = 0; k < {DC}; ++k) bv[k] = 0.f; }}")
+                for q in range(Q):
+                    w("        {  // one check copy at a time: the state owns the registers")
+                    w(f"            float m[{DC}];")
+                    w(f"            int ro = {(e0 - e0c) * Z + q * ZT} + u;  // one base VGPR per row copy: the edges ride in")
+                    w("            asm volatile(\"\" : \"+v\"(ro));  // the 16-bit DS offset")
+                    w("            float* rq = lds + ro;")
+                    for k, e in enumerate(es):
+                        if e in d1set:
+                            w(f"            if constexpr (D1_BYPASS) m[{k}] = cd[{S.cd_index[p].index((e, q))}]; "
+                              f"else m[{k}] = rq[{k * Z}];")
+                        else:
+                            w(f"            m[{k}] = rq[{k * Z}];")
+                    w(f"            cn_copy<KIND, {DC}>(m, wv, bv, a, wc != nullptr);")
+                    for k, e in enumerate(es):
+                        if e in d1set:
+                            j = int(S.hb_cols[e])
+                            c, dv = rot(e, q)
+                            w("            if constexpr (D1_BYPASS) {")
+                            w(f"                const uint32_t dv_ = {dv};")
+                            w(f"                bstore(nr, vo + dv_, {4 * (j * Z + c)}, "
+                              f"fadd(cd[{S.cd_index[p].index((e, q))}], fadd(0.f, m[{k}])));")
+                            w(f"                if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m[{k}]);")
+                            w(f"            }} else {{ rq[{k * Z}] = m[{k}]; }}")
+                        else:
+                            w(f"            rq[{k * Z}] = m[{k}];")
+                    w("        }")
+                    if Q > 1:
+                        w("        __builtin_amdgcn_sched_barrier(0);")
+                w("    }")
+            w("}")
 
     # ---------------------------------------------------------------- the kernel
     def each_part(fmt, indent="        "):
@@ -392,6 +412,15 @@ def emit(S: Spec) -> str:
         for n, j in enumerate(S.d1_cols[p]):
             for q in range(Q):
                 w(f"    xd[{n * Q + q}] = bload(xr, vo, {X(j, q)});")
+        ncd = max(len(S.cd_index[p]), 1)
+        w(f"    float cd[{ncd}];  // D1_BYPASS: xa of the degree-1 edges of this part's check rows, rotated copies")
+        w("    if constexpr (D1_BYPASS) {")
+        for idx, (e, q) in enumerate(S.cd_index[p]):
+            c, dv = rot(e, q)
+            w(f"        cd[{idx}] = bload(xr, vo + {dv}, {4 * (int(S.hb_cols[e]) * Z + c)});")
+        w("    } else {")
+        w(f"        for (int k = 0; k < {ncd}; ++k) cd[k] = 0.f;")
+        w("    }")
         # cumulative VN weighting: the channel registers hold xin and advance one step per iteration
         def chan_steps(step_expr, indent):
             w(f"{indent}{{ const cfloat_p wr_ = (cfloat_p)(a.w_vn + (int64_t)({step_expr}) * N);")
@@ -454,8 +483,7 @@ def emit(S: Spec) -> str:
             stamp(2 + 3 * ci)
             w("        __syncthreads();")
             if "cn" not in SKIP:
-                for dc, t0, n in S.cn_groups[(p, ci)]:
-                    w(f"        cn_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]});")
+                w(f"        cn_p{p}_c{ci}<KIND, SAVE>(lds, u, a, it, cd, vo, nr, cr, vc, co_last);")
             stamp(3 + 3 * ci)
             w("        __syncthreads();")
             w(f"        rd_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm);")
@@ -494,6 +522,7 @@ def emit(S: Spec) -> str:
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
     each_part("run_p{p}<KIND, SAVE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm)", indent="    ")
     w("}")
+    w("#undef D1_BYPASS")
     w("}  // namespace")
     return "\n".join(L)
 

@@ -192,6 +192,22 @@ __device__ __forceinline__ float wave_sum(float x) {
     return x;
 }
 
+// check node of one check copy in place (m: gathered v2c -> c2v), every kind: Neural through the
+// specialised neural_row, the Boosted kinds through the shared cn_core + cn_epilogue
+template <int KIND, int DC>
+__device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], const float (&bv)[DC],
+                                        const FusedArgs& a, bool has_w) {
+    if constexpr (KIND == NLDPC_NEURAL) {
+        neural_row<DC>(m, wv, bv);
+    } else {
+        CnCore<DC> core;
+        cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core);
+#pragma unroll
+        for (int k = 0; k < DC; ++k)
+            m[k] = cn_epilogue<KIND, false>(core.out0[k], wv[k], 0.f, 0.f, 0.f, has_w, false, a.qbit, a.lo, a.hi).c;
+    }
+}
+
 struct FusedSpec {
     const char* tag;
     int32_t M, N, Z, E, G, threads;
