@@ -30,6 +30,8 @@ SKIP = set(filter(None, os.environ.get("NLDPC_GEN_SKIP", "").split(",")))  # deb
 # kernels, lane 0 of each wave, first 256 workgroups (FusedArgs::stamps, tools/stamps.py)
 STAMPS = os.environ.get("NLDPC_GEN_STAMPS") == "1"
 LDS_BYTES = 160 * 1024 - 2048  # leave room for the compiler / alignment
+# check rows up to this degree let the compiler interleave their lane copies (more ILP, more registers)
+CN_PAIR_MAXDC = int(os.environ.get("NLDPC_GEN_CNPAIR", "0"))
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q)
 SPECS = [
@@ -318,6 +320,12 @@ def emit(S: Spec) -> str:
                             lst.append((e, q))
         S.cd_index[p] = lst
 
+    S.cn_order, S.cn_nw = {}, {}
+    for p in range(S.P):
+        for ci in range(len(S.chunks)):
+            S.cn_order[(p, ci)] = sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i]))
+            S.cn_nw[(p, ci)] = max(sum(len(S.row_edges[i]) for i in S.cn_order[(p, ci)]), 1)
+
     def rot(e, q):  # check copy h = u + q*ZT of edge e sits at variable copy (u + c) mod Z
         c = (q * ZT + int(S.shift[e])) % Z
         dv = f"(u >= {Z - c} ? {(-4 * Z) & 0xFFFFFFFF}u : 0u)" if c + ZT > Z else "0u"
@@ -328,21 +336,18 @@ def emit(S: Spec) -> str:
         for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
             w("template <int KIND, bool SAVE>")
             w(f"__device__ __forceinline__ void cn_p{p}_c{ci}(float* lds, int u, const FusedArgs& a, int it, "
-              f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last) {{")
+              f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last, "
+              f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}]) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
-            rows = sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i]))
-            for i in rows:
+            wo = 0
+            for i in S.cn_order[(p, ci)]:
                 es = S.row_edges[i]
                 DC, e0 = len(es), es[0]
-                w(f"    {{  // check row {i}: edges {e0}..{e0 + DC - 1}")
+                w(f"    {{  // check row {i}: edges {e0}..{e0 + DC - 1}; weights preloaded (W/Bv[{wo}..])")
                 w(f"        float wv[{DC}], bv[{DC}];")
-                w(f"        const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + {e0}) : nullptr;")
-                w(f"        const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + {e0}) : nullptr;")
-                w("        // whole-row scalar loads (one uniform test per row, not per edge, so the loads can merge)")
-                w(f"        if (KIND == NLDPC_NEURAL || wc) {{ for (int k = 0; k < {DC}; ++k) wv[k] = wc[k]; }}")
-                w(f"        else {{ for (int k = 0; k < {DC}; ++k) wv[k] = 1.f; }}")
-                w(f"        if (KIND == NLDPC_NEURAL || bs) {{ for (int k = 0; k < {DC}; ++k) bv[k] = bs[k]; }}")
-                w(f"        else {{ for (int k = 0; k < {DC}; ++k) bv[k] = 0.f; }}")
+                w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{wo} + k]; bv[k] = Bv[{wo} + k]; }}")
+                w("        const bool wc = a.w_cn != nullptr;")
+                wo += DC
                 for q in range(Q):
                     w("        {  // one check copy at a time: the state owns the registers")
                     w(f"            float m[{DC}];")
@@ -355,7 +360,7 @@ def emit(S: Spec) -> str:
                               f"else m[{k}] = rq[{k * Z}];")
                         else:
                             w(f"            m[{k}] = rq[{k * Z}];")
-                    w(f"            cn_copy<KIND, {DC}>(m, wv, bv, a, wc != nullptr);")
+                    w(f"            cn_copy<KIND, {DC}>(m, wv, bv, a, wc);")
                     for k, e in enumerate(es):
                         if e in d1set:
                             j = int(S.hb_cols[e])
@@ -369,7 +374,7 @@ def emit(S: Spec) -> str:
                         else:
                             w(f"            rq[{k * Z}] = m[{k}];")
                     w("        }")
-                    if Q > 1:
+                    if Q > 1 and DC > CN_PAIR_MAXDC:
                         w("        __builtin_amdgcn_sched_barrier(0);")
                 w("    }")
             w("}")
@@ -479,11 +484,32 @@ def emit(S: Spec) -> str:
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
         stamp(1)
         for ci in range(len(S.chunks)):
+            nw = S.cn_nw[(p, ci)]
+            # this chunk's check-node weights, by whole-row scalar loads issued before the write phase
+            # (their latency overlaps the LDS writes and the barrier, not the check rows' LDS waits)
+            w(f"        float W{ci}[{nw}], B{ci}[{nw}];")
+            w("        {")
+            w("            const cfloat_p wc_ = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E) : nullptr;")
+            w("            const cfloat_p bs_ = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E) : nullptr;")
+            wo, wl, bl = 0, [], []
+            for i in S.cn_order[(p, ci)]:
+                for k, e in enumerate(S.row_edges[i]):
+                    wl.append(f"W{ci}[{wo}] = wc_[{e}];")
+                    bl.append(f"B{ci}[{wo}] = bs_[{e}];")
+                    wo += 1
+            if "wload" in SKIP:  # timing experiment only: constant weights, no scalar loads
+                w(f"            for (int k = 0; k < {nw}; ++k) {{ W{ci}[k] = 0.5f; B{ci}[k] = 0.f; }}")
+            else:
+                w(f"            if (KIND == NLDPC_NEURAL || wc_) {{ {' '.join(wl)} }}")
+                w(f"            else {{ for (int k = 0; k < {nw}; ++k) W{ci}[k] = 1.f; }}")
+                w(f"            if (KIND == NLDPC_NEURAL || bs_) {{ {' '.join(bl)} }}")
+                w(f"            else {{ for (int k = 0; k < {nw}; ++k) B{ci}[k] = 0.f; }}")
+            w("        }")
             w(f"        wr_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, it, sv, vc);")
             stamp(2 + 3 * ci)
             w("        __syncthreads();")
             if "cn" not in SKIP:
-                w(f"        cn_p{p}_c{ci}<KIND, SAVE>(lds, u, a, it, cd, vo, nr, cr, vc, co_last);")
+                w(f"        cn_p{p}_c{ci}<KIND, SAVE>(lds, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci});")
             stamp(3 + 3 * ci)
             w("        __syncthreads();")
             w(f"        rd_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm);")
