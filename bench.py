@@ -356,10 +356,15 @@ def cpu_baseline(bg, Z, T, sigma, target_s):
             neural_forward(g, x, w, bb)
         return time.perf_counter() - t0
 
-    b = 2
-    t = run(b)
-    b2 = int(max(2, min(512, b * target_s / max(t, 1e-3))))
-    if b2 > b:
+    # scale the sample until it takes about target_s (per-call overheads make small batches slow per
+    # codeword, so one extrapolation from b=2 undershoots)
+    b, t = 2, run(2)
+    for _ in range(3):
+        if t >= 0.6 * target_s:
+            break
+        b2 = int(max(b + 1, min(2048, b * target_s / max(t, 1e-3))))
+        if b2 <= b:
+            break
         b, t = b2, run(b2)
     cpu_name = ""
     try:
