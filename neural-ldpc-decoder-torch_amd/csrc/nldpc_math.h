@@ -61,6 +61,18 @@ __device__ __forceinline__ float quantize(float x, int q) {
     return active ? r : x;
 }
 
+// The same quantiser in four operations when q is active: clamp(rint(x*s), +-hi*s) * inv.  Equal to
+// quantize() for every non-NaN x: the STE form xc + (qv - xc) is exactly qv (|qv - xc| is below the
+// grid step, so the difference is exact and so is the sum), and clamping commutes with the exact
+// power-of-two scalings (checked exhaustively over random and boundary inputs for every q).
+__device__ __forceinline__ float quantize_active(float x, int q) {
+    const float s = q == 5 ? 2.f : (q == 3 ? 0.5f : 1.f);
+    const float inv = q == 5 ? 0.5f : (q == 3 ? 2.f : 1.f);
+    const float hs = q == 6 ? 15.5f : (q == 5 ? 15.f : (q == -5 ? 15.f : (q == 4 ? 7.f : 3.f)));  // hi * s
+    return fmul(__builtin_amdgcn_fmed3f(rintf(fmul(x, s)), -hs, hs), inv);
+}
+__device__ __forceinline__ bool qms_active_q(int q) { return q == 6 || q == 5 || q == -5 || q == 4 || q == 3; }
+
 // QMS training state.  The backward reads a saved v2c message m only through Q(m) and the STE mask of
 // Q's clip on m, so QMS saves one signed byte 2*m' per message: m' = Q(m) inside the clip range and
 // sign(m) * (hi + 1) outside it, which gives Q(m') == Q(m) and the same mask (Q's values are
