@@ -372,7 +372,8 @@ __device__ __forceinline__ void cn_backward(const float (&m)[DC], const float (&
 // Register-light min-sum backward of one check copy (MS / QMS / Neural) for the fused backward
 // kernels: cn_backward's arithmetic (same operations, same order, same results) restructured into
 // three passes over the edges so that only the two minima and per-edge bit masks stay live between
-// them.  load_m(k) gives edge k's v2c input; lds[k * stride] holds dL/dc2v on entry and receives
+// them.  load_m(k) gives edge k's v2c input (QMS: the decoded int8 code of the saved state, with an
+// active quantiser); lds[k * stride] holds dL/dc2v on entry and receives
 // dL/dv2c.  gwa / gba accumulate this copy's dL/dw_cn and dL/dbias contributions.
 template <int DC, int KIND, typename LoadM>
 __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride, const float (&wc)[DC],
@@ -386,11 +387,13 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
     for (int k = 0; k < DC; ++k) {  // pass 1: conditioned inputs, minima, signs, STE masks
         float x = load_m(k);
         bool msk = true;
-        if (KIND == NLDPC_QMS && qr.active) msk = x >= qr.lo && x <= qr.hi;
+        if (KIND == NLDPC_QMS) msk = x >= qr.lo && x <= qr.hi;
         if (KIND == NLDPC_MS) msk = x >= lo && x <= hi;
-        if (KIND == NLDPC_QMS) x = quantize(x, qbit);
-        if (KIND == NLDPC_MS) x = clampf(x, lo, hi);
-        if (KIND != NLDPC_NEURAL) x = fadd(x, fmul(kZeroFix, (fabsf(x) > 0.f) ? 0.f : 1.f));
+        // QMS inputs are decoded int8 codes (qms_code): on the quantiser's grid inside the clip range,
+        // +-(hi + 1) outside it, so Q(m) is a clamp
+        if (KIND == NLDPC_QMS) x = __builtin_amdgcn_fmed3f(x, qr.lo, qr.hi);
+        if (KIND == NLDPC_MS) x = __builtin_amdgcn_fmed3f(x, lo, hi);
+        if (KIND != NLDPC_NEURAL) x = x == 0.f ? kZeroFix : x;
         const float ax = fabsf(x);
         const uint32_t pos = x > 0.f;
         npos ^= pos;
