@@ -67,7 +67,7 @@ __device__ __forceinline__ int block_slot() { return blockIdx.x * gridDim.z + bl
 // Sum of one value over the workgroup, stored by thread 0 into dst[block_slot() * width].  Every
 // thread of the block calls it (uniform control flow).
 __device__ __forceinline__ void block_partial(float v, float* dst, int width, float* lds) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    v = wave_sum(v);  // DPP reduction (nldpc_fused.h)
     const int tid = threadIdx.y * blockDim.x + threadIdx.x;
     const int nw = (blockDim.x * blockDim.y + 63) >> 6;
     if ((tid & 63) == 0) lds[tid >> 6] = v;
@@ -94,8 +94,7 @@ __device__ __forceinline__ void block_edge_partials(float (&v)[NA][DC], int d, f
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             if (k < d) {
-                float x = v[a][k];
-                for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+                const float x = wave_sum(v[a][k]);
                 if ((tid & 63) == 0) lds[(wv * NA + a) * DC + k] = x;
             }
         }

@@ -186,24 +186,22 @@ __device__ __forceinline__ float gy_masked(rsrc_t gr, rsrc_t mr, uint32_t vo, ui
     if (KIND == NLDPC_NEURAL) return g;
     return bload8(mr, vm, so >> 2) ? g : 0.f;
 }
-// Sum over the 64 lanes of a wave, every lane gets it: DPP within rows of 16 (quad permutes, then the
-// half-row and row mirrors) and the gfx950 permlane swaps across rows -- all VALU, no LDS traffic
-// (__shfl_xor would issue six ds_bpermute per sum).
-template <int CTRL>
+// Sum over the 64 lanes of a wave (wave-uniform result): DPP within rows of 16 (quad permutes, then the
+// half-row and row mirrors), then the gfx9 row broadcasts 15 / 31 carry the row sums up to lane 63,
+// read back with v_readlane -- all VALU, no LDS traffic (__shfl_xor issues a ds_bpermute per step).
+template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ float dpp_mov(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+    return __builtin_bit_cast(float,
+                              __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROW_MASK, 0xf, false));
 }
 __device__ __forceinline__ float wave_sum(float x) {
-    x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]
-    x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]: quad sums
-    x += dpp_mov<0x141>(x);  // row_half_mirror: 8-lane sums
-    x += dpp_mov<0x140>(x);  // row_mirror: every lane holds its row's (16-lane) sum
-    const auto a = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, x), __builtin_bit_cast(uint32_t, x),
-                                                    false, false);
-    x = __builtin_bit_cast(float, a[0]) + __builtin_bit_cast(float, a[1]);  // rows 0+1 | 2+3
-    const auto b = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, x), __builtin_bit_cast(uint32_t, x),
-                                                    false, false);
-    return __builtin_bit_cast(float, b[0]) + __builtin_bit_cast(float, b[1]);
+    x += dpp_mov<0xB1>(x);        // quad_perm [1,0,3,2]
+    x += dpp_mov<0x4E>(x);        // quad_perm [2,3,0,1]: quad sums
+    x += dpp_mov<0x141>(x);       // row_half_mirror: 8-lane sums
+    x += dpp_mov<0x140>(x);       // row_mirror: every lane holds its row's (16-lane) sum
+    x += dpp_mov<0x142, 0xa>(x);  // row_bcast:15 into rows 1, 3: rows 0+1 | 2+3
+    x += dpp_mov<0x143, 0xc>(x);  // row_bcast:31 into rows 2, 3: lane 63 = the wave's sum
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
 
 // Boosted MS / QMS (active quantiser) check node of one check copy in place, specialised like
