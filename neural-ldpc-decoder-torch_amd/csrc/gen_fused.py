@@ -32,6 +32,10 @@ STAMPS = os.environ.get("NLDPC_GEN_STAMPS") == "1"
 LDS_BYTES = 160 * 1024 - 2048  # leave room for the compiler / alignment
 # check rows up to this degree let the compiler interleave their lane copies (more ILP, more registers)
 CN_PAIR_MAXDC = int(os.environ.get("NLDPC_GEN_CNPAIR", "0"))
+# VN lane copies as packed fp32 pairs (v_pk_add_f32) or all scalar chains.  Measured on gfx950 (stamp
+# build): a v_pk_add_f32 occupies the SIMD for 8 cycles against 2 for v_add_f32, so packing costs
+# time per element; scalar is the default
+PACK_VN = os.environ.get("NLDPC_GEN_PACK") == "1"
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q)
 SPECS = [
@@ -112,18 +116,19 @@ def emit(S: Spec) -> str:
     # additions run as packed fp32 (v_pk_add_f32: two IEEE adds per lane, same rounding); an odd
     # copy count leaves one scalar array.  The channel values a thread needs every iteration are
     # loaded once into registers (xp*/xs for its register columns, xd for its degree-1 columns).
-    NPAIR, SINGLE = Q // 2, Q % 2
+    NPAIR = Q // 2 if PACK_VN else 0
+    NSINGLE = Q - 2 * NPAIR
 
     def ref(q, k):
         if q < 2 * NPAIR:
             return f"cp{q // 2}[{k}].{'x' if q % 2 == 0 else 'y'}"
-        return f"cs[{k}]"
+        return f"cs{q - 2 * NPAIR}[{k}]"
 
     def xref(p, j, q):
         cols = S.reg_cols[p]
         if j in cols:
             n = cols.index(j)
-            return f"xp{q // 2}[{n}].{'x' if q % 2 == 0 else 'y'}" if q < 2 * NPAIR else f"xs[{n}]"
+            return f"xp{q // 2}[{n}].{'x' if q % 2 == 0 else 'y'}" if q < 2 * NPAIR else f"xs{q - 2 * NPAIR}[{n}]"
         n = S.d1_cols[p].index(j)
         return f"xd[{n * Q + q}]"
 
@@ -131,23 +136,23 @@ def emit(S: Spec) -> str:
         sp = len(S.slots[p])
         c = "const " if const else ""
         ps = [f"{c}f2 (&cp{i})[{max(sp, 1)}]" for i in range(NPAIR)]
-        if SINGLE:
-            ps.append(f"{c}float (&cs)[{max(sp, 1)}]")
+        for i in range(NSINGLE):
+            ps.append(f"{c}float (&cs{i})[{max(sp, 1)}]")
         return ", ".join(ps)
 
     def state_args():
-        return ", ".join([f"cp{i}" for i in range(NPAIR)] + (["cs"] if SINGLE else []))
+        return ", ".join([f"cp{i}" for i in range(NPAIR)] + [f"cs{i}" for i in range(NSINGLE)])
 
     def x_params(p):
         nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
         ps = [f"const f2 (&xp{i})[{nr}]" for i in range(NPAIR)]
-        if SINGLE:
-            ps.append(f"const float (&xs)[{nr}]")
+        for i in range(NSINGLE):
+            ps.append(f"const float (&xs{i})[{nr}]")
         ps.append(f"const float (&xd)[{nd}]")
         return ", ".join(ps)
 
     def x_args():
-        return ", ".join([f"xp{i}" for i in range(NPAIR)] + (["xs"] if SINGLE else []) + ["xd"])
+        return ", ".join([f"xp{i}" for i in range(NPAIR)] + [f"xs{i}" for i in range(NSINGLE)] + ["xd"])
 
     # ---------------------------------------------------------------- variable nodes
     # global accesses: bload/bstore(descriptor, lane byte offset vo, constant byte offset)
@@ -161,8 +166,8 @@ def emit(S: Spec) -> str:
         puts an s_nop between two dependent packed adds).  Each chain is the reference's sequential
         fp32 order: S_k = ((P_{k-1} + c_{k+1}) + ...) + c_{d-1}, v2c_k = x0 + S_k, P_k = P_{k-1} + c_k."""
         grp = [("f2", f"cp{i}", f"xp{i}[{n}]", str(i)) for i in range(NPAIR)]
-        if SINGLE:
-            grp.append(("float", "cs", f"xs[{n}]", "s"))
+        for i in range(NSINGLE):
+            grp.append(("float", f"cs{i}", f"xs{i}[{n}]", f"s{i}"))
 
         def add(T_, x, y):
             return f"({x} + {y})" if T_ == "f2" else f"fadd({x}, {y})"
@@ -177,21 +182,41 @@ def emit(S: Spec) -> str:
             for T_, arr, xin, g in grp:
                 ch = f"chan2<KIND>({xin}, a)" if T_ == "f2" else f"chan<KIND>({xin}, a)"
                 w(f"            const {T_} x0_{g} = {add(T_, zero(T_), ch)};")
-            for k in range(d):
+            # edges two at a time: the chains of k and k+1 (S_k from P_{k-1}, S_{k+1} from P_k) run
+            # interleaved -- twice the independent adds per wave for the VN's dependent-add tail.
+            # Chain k reads c_{k+1} first, before chain k+1 overwrites it with v2c_{k+1}.
+            for k in range(0, d, 2):
+                two = k + 1 < d
                 w("            {")
-                for T_, arr, xin, g in grp:
-                    w(f"                {T_} S_{g} = P_{g};")
-                for m in range(k + 1, d):
+                if two:
                     for T_, arr, xin, g in grp:
-                        w(f"                S_{g} = {add(T_, f'S_{g}', f'{arr}[{s + m}]')};")
-                for T_, arr, xin, g in grp:
-                    w(f"                const {T_} o_{g} = {arr}[{s + k}]; {arr}[{s + k}] = {add(T_, f'x0_{g}', f'S_{g}')};")
-                # the fake dependence of the running prefix on the new message keeps the compiler from
-                # running the prefix chain ahead and holding every partial sum in a register
-                for T_, arr, xin, g in grp:
-                    w(f"                asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]));")
-                for T_, arr, xin, g in grp:
-                    w(f"                P_{g} = {add(T_, f'P_{g}', f'o_{g}')};")
+                        w(f"                const {T_} Pk_{g} = {add(T_, f'P_{g}', f'{arr}[{s + k}]')};  // P_k")
+                    for T_, arr, xin, g in grp:
+                        w(f"                {T_} S_{g} = {add(T_, f'P_{g}', f'{arr}[{s + k + 1}]')};")
+                        w(f"                {T_} U_{g} = Pk_{g};")
+                    for m in range(k + 2, d):
+                        for T_, arr, xin, g in grp:
+                            w(f"                S_{g} = {add(T_, f'S_{g}', f'{arr}[{s + m}]')};")
+                            w(f"                U_{g} = {add(T_, f'U_{g}', f'{arr}[{s + m}]')};")
+                    for T_, arr, xin, g in grp:
+                        w(f"                const {T_} o_{g} = {arr}[{s + k + 1}];")
+                        w(f"                {arr}[{s + k}] = {add(T_, f'x0_{g}', f'S_{g}')}; "
+                          f"{arr}[{s + k + 1}] = {add(T_, f'x0_{g}', f'U_{g}')};")
+                    # the fake dependence of the running prefix on the new messages keeps the compiler
+                    # from running the prefix chain ahead and holding every partial sum in a register
+                    for T_, arr, xin, g in grp:
+                        w(f"                asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]), \"v\"({arr}[{s + k + 1}]));")
+                    for T_, arr, xin, g in grp:
+                        w(f"                P_{g} = {add(T_, f'Pk_{g}', f'o_{g}')};")
+                else:
+                    for T_, arr, xin, g in grp:
+                        w(f"                {T_} S_{g} = P_{g};")
+                    for T_, arr, xin, g in grp:
+                        w(f"                const {T_} o_{g} = {arr}[{s + k}]; {arr}[{s + k}] = {add(T_, f'x0_{g}', f'S_{g}')};")
+                    for T_, arr, xin, g in grp:
+                        w(f"                asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]));")
+                    for T_, arr, xin, g in grp:
+                        w(f"                P_{g} = {add(T_, f'P_{g}', f'o_{g}')};")
                 w("            }")
         else:
             for k in range(d):
@@ -225,15 +250,16 @@ def emit(S: Spec) -> str:
                     w(f"                bstore(pr, vo, {X(j, 2 * i + 1)}, y_.y);")
                     w("            }")
                     w("            }")
-                if SINGLE:
+                for i in range(NSINGLE):
+                    q = 2 * NPAIR + i
                     w("            {")
-                    w(f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, Q - 1)}) : xs[{n}];")
+                    w(f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : xs{i}[{n}];")
                     w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w("                bool m_;")
-                    w(f"                bstore(pr, vo, {X(j, Q - 1)}, posterior_m<KIND>(xo_, P_s, a, m_));")
-                    w(f"                bstore8(pm, vm, {X(j, Q - 1) // 4}, m_);")
+                    w(f"                bstore(pr, vo, {X(j, q)}, posterior_m<KIND>(xo_, P_s{i}, a, m_));")
+                    w(f"                bstore8(pm, vm, {X(j, q) // 4}, m_);")
                     w("            } else {")
-                    w(f"                bstore(pr, vo, {X(j, Q - 1)}, posterior<KIND>(xo_, P_s, a));")
+                    w(f"                bstore(pr, vo, {X(j, q)}, posterior<KIND>(xo_, P_s{i}, a));")
                     w("            }")
                     w("            }")
                 w("        }")
@@ -398,22 +424,22 @@ def emit(S: Spec) -> str:
           f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm) {{")
         for i in range(NPAIR):
             w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
-        if SINGLE:
-            w(f"    float cs[{sp}], xs[{nr}];")
+        for i in range(NSINGLE):
+            w(f"    float cs{i}[{sp}], xs{i}[{nr}];")
         w(f"    float xd[{nd}];")
         w("#pragma unroll")
         w(f"    for (int k = 0; k < {sp}; ++k) {{")
         for i in range(NPAIR):
             w(f"        cp{i}[k] = f2{{0.f, 0.f}};")
-        if SINGLE:
-            w("        cs[k] = 0.f;")
+        for i in range(NSINGLE):
+            w(f"        cs{i}[k] = 0.f;")
         w("    }")
         w("    // this thread's channel values, loaded once for all T iterations")
         for n, j in enumerate(S.reg_cols[p]):
             for i in range(NPAIR):
                 w(f"    xp{i}[{n}] = f2{{bload(xr, vo, {X(j, 2 * i)}), bload(xr, vo, {X(j, 2 * i + 1)})}};")
-            if SINGLE:
-                w(f"    xs[{n}] = bload(xr, vo, {X(j, Q - 1)});")
+            for i in range(NSINGLE):
+                w(f"    xs{i}[{n}] = bload(xr, vo, {X(j, 2 * NPAIR + i)});")
         for n, j in enumerate(S.d1_cols[p]):
             for q in range(Q):
                 w(f"    xd[{n * Q + q}] = bload(xr, vo, {X(j, q)});")
@@ -433,8 +459,8 @@ def emit(S: Spec) -> str:
                 for i in range(NPAIR):
                     for c in "xy":
                         w(f"{indent}  xp{i}[{n}].{c} = chan_step<KIND>(xp{i}[{n}].{c}, a, wr_[{j}]);")
-                if SINGLE:
-                    w(f"{indent}  xs[{n}] = chan_step<KIND>(xs[{n}], a, wr_[{j}]);")
+                for i in range(NSINGLE):
+                    w(f"{indent}  xs{i}[{n}] = chan_step<KIND>(xs{i}[{n}], a, wr_[{j}]);")
             for n, j in enumerate(S.d1_cols[p]):
                 for q in range(Q):
                     w(f"{indent}  xd[{n * Q + q}] = chan_step<KIND>(xd[{n * Q + q}], a, wr_[{j}]);")
