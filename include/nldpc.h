@@ -141,6 +141,18 @@ int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_
 int nldpc_ber_count(const float* llr, const uint8_t* y, int64_t B, int64_t L, int32_t convention,
                     int64_t* counts, void* stream);
 
+/* ---- count-only decode (§8 F2): nldpc_forward followed by nldpc_ber_count on every iteration's
+ *      output (the test loop of test/test_*.py around Functions.evaluate_ber_fer, Functions.py:85-102),
+ *      fused into the decoder: each iteration's posterior is compared with the codeword bit inside
+ *      the register-resident kernel and only the counts leave the chip (no T x [B][N*Z] outputs).
+ *   arguments as nldpc_forward (no outs / app_prev / c2v / v2c / saved); y [B][N*Z] uint8 bits or
+ *   NULL (all-zero codeword); counts int64 [T][2] device, += (bit errors, frame errors) of iteration
+ *   first_iter + k in row k; convention as nldpc_ber_count.  Needs the fused path (nldpc_fast_path
+ *   with saving = 0 reports 1), NLDPC_EUNSUPPORTED otherwise. */
+int nldpc_forward_count(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
+                        const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
+                        const uint8_t* y, int32_t convention, int64_t* counts, void* stream);
+
 /* ---- multi-iteration BCE loss (config 5's training loss): replaces LDPCDecoderLoss.forward with
  *      LossType.BCE over a list of outputs and one label tensor
  *      (src/boosted_neural_ldpc_decoder/LDPCDecoderLoss.py:70-108, binary_cross_entropy_with_logits

@@ -110,7 +110,14 @@ def emit(S: Spec) -> str:
     w(f"namespace fused_{S.tag} {{")
     w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E};")
     w("// degree-1 edges bypass LDS (Neural inference; see the check-node section)")
+    # MODE 0: decode, MODE 1: decode and save what the backward needs, MODE 2 / 3: count-only decode
+    # (the posteriors are compared with the all-zero codeword / the codeword y and counted instead of
+    # stored)
+    w("#define SAVE (MODE == 1)")
+    w("#define CNT (MODE >= 2)")
+    w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
     w("#define D1_BYPASS (KIND == NLDPC_NEURAL && !SAVE)")
+    assert NZ < 65536  # per-codeword error counts are packed two to an LDS word
 
     # Register state of part p: copies are paired (q = 0,1 / 2,3 ...) into float2 arrays so the VN's
     # additions run as packed fp32 (v_pk_add_f32: two IEEE adds per lane, same rounding); an odd
@@ -227,9 +234,9 @@ def emit(S: Spec) -> str:
         cols = S.reg_cols[p]
         for final in (False, True):
             fname = f"post_p{p}" if final else f"vn_p{p}"
-            w("template <int KIND, bool SAVE>")
+            w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void {fname}({state_params(p)}, {x_params(p)}, const FusedArgs& a, "
-              f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm) {{")
+              f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps) {{")
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
@@ -246,8 +253,8 @@ def emit(S: Spec) -> str:
                     w(f"                bstore8(pm, vm, {X(j, 2 * i + 1) // 4}, m1_);")
                     w("            } else {")
                     w(f"                const f2 y_ = posterior2<KIND>(xo_, P_{i}, a);")
-                    w(f"                bstore(pr, vo, {X(j, 2 * i)}, y_.x);")
-                    w(f"                bstore(pr, vo, {X(j, 2 * i + 1)}, y_.y);")
+                    w(f"                put_post<CM>(pr, vo, {X(j, 2 * i)}, y_.x, ps);")
+                    w(f"                put_post<CM>(pr, vo, {X(j, 2 * i + 1)}, y_.y, ps);")
                     w("            }")
                     w("            }")
                 for i in range(NSINGLE):
@@ -259,7 +266,7 @@ def emit(S: Spec) -> str:
                     w(f"                bstore(pr, vo, {X(j, q)}, posterior_m<KIND>(xo_, P_s{i}, a, m_));")
                     w(f"                bstore8(pm, vm, {X(j, q) // 4}, m_);")
                     w("            } else {")
-                    w(f"                bstore(pr, vo, {X(j, q)}, posterior<KIND>(xo_, P_s{i}, a));")
+                    w(f"                put_post<CM>(pr, vo, {X(j, q)}, posterior<KIND>(xo_, P_s{i}, a), ps);")
                     w("            }")
                     w("            }")
                 w("        }")
@@ -282,7 +289,7 @@ def emit(S: Spec) -> str:
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
             mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
             d1 = [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
-            w("template <int KIND, bool SAVE>")
+            w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void wr_p{p}_c{ci}({state_params(p, True)}, {x_params(p)}, float* lds, "
               f"int u, const FusedArgs& a, int it, rsrc_t sv, uint32_t vc) {{")
             w("    asm volatile(\"\" : \"+v\"(u));  // LDS addresses are recomputed here, not hoisted out of the loop")
@@ -299,10 +306,10 @@ def emit(S: Spec) -> str:
             if d1:
                 w("    }")
             w("}")
-            w("template <int KIND, bool SAVE>")
+            w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
               f"int u, const FusedArgs& a, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co, "
-              f"uint32_t vm, rsrc_t xr, rsrc_t pm) {{")
+              f"uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
             for q in range(Q):
                 for k, e in mine:
@@ -316,7 +323,7 @@ def emit(S: Spec) -> str:
                     w("      if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w(f"          bool m_; bstore(pr, vo, {X(j, q)}, posterior_m<KIND>(xo_, P_, a, m_)); "
                       f"bstore8(pm, vm, {X(j, q) // 4}, m_);")
-                    w(f"      }} else {{ bstore(pr, vo, {X(j, q)}, posterior<KIND>(xo_, P_, a)); }} }}")
+                    w(f"      }} else {{ put_post<CM>(pr, vo, {X(j, q)}, posterior<KIND>(xo_, P_, a), ps); }} }}")
             if d1:
                 w("    if (has_co) {  // final message state (last iteration only)")
                 for j, e in d1:
@@ -360,10 +367,10 @@ def emit(S: Spec) -> str:
     for p in range(S.P):
         ncd = max(len(S.cd_index[p]), 1)
         for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
-            w("template <int KIND, bool SAVE>")
+            w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void cn_p{p}_c{ci}(float* lds, int u, const FusedArgs& a, int it, "
               f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last, "
-              f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}]) {{")
+              f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
             wo = 0
             for i in S.cn_order[(p, ci)]:
@@ -393,8 +400,8 @@ def emit(S: Spec) -> str:
                             c, dv = rot(e, q)
                             w("            if constexpr (D1_BYPASS) {")
                             w(f"                const uint32_t dv_ = {dv};")
-                            w(f"                bstore(nr, vo + dv_, {4 * (j * Z + c)}, "
-                              f"fadd(cd[{S.cd_index[p].index((e, q))}], fadd(0.f, m[{k}])));")
+                            w(f"                put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, "
+                              f"fadd(cd[{S.cd_index[p].index((e, q))}], fadd(0.f, m[{k}])), ps);")
                             w(f"                if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m[{k}]);")
                             w(f"            }} else {{ rq[{k * Z}] = m[{k}]; }}")
                         else:
@@ -414,14 +421,16 @@ def emit(S: Spec) -> str:
     # part's at a control-flow join (per-phase part branches inside one loop made the register
     # allocator insert phi copies and spill).  The parts still meet at every s_barrier: a hardware
     # barrier counts waves, not program counters, and every part executes the same barrier sequence.
+    # this thread's codeword counters (recomputed at each flush: no register held across the iteration)
+    cnt_slot = "cntl" if G == 1 else f"cntl + (int)((threadIdx.x % {S.lanes}) / {ZT}) * 32"
     for p in range(S.P):
         if PARTS and p not in PARTS:
             continue
         sp = max(len(S.slots[p]), 1)
         nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
-        w("template <int KIND, bool SAVE>")
+        w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
-          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm) {{")
+          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl) {{")
         for i in range(NPAIR):
             w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
         for i in range(NSINGLE):
@@ -443,6 +452,8 @@ def emit(S: Spec) -> str:
         for n, j in enumerate(S.d1_cols[p]):
             for q in range(Q):
                 w(f"    xd[{n * Q + q}] = bload(xr, vo, {X(j, q)});")
+        w(f"    PostSink ps{{make_rsrc((const float*)(a.cnt_y ? a.cnt_y + blk * {NZ} : nullptr), "
+          f"a.cnt_y ? nlive * {NZ} : 0), 0, a.cnt_conv}};")
         ncd = max(len(S.cd_index[p]), 1)
         w(f"    float cd[{ncd}];  // D1_BYPASS: xa of the degree-1 edges of this part's check rows, rotated copies")
         w("    if constexpr (D1_BYPASS) {")
@@ -498,7 +509,9 @@ def emit(S: Spec) -> str:
         w("        const uint8_t* pmp = (SAVE && a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t pm = make_rsrc((const float*)(pmp ? pmp + blk * {NZ} : nullptr), pmp ? nlive * {NZ} : 0);")
         if "vn" not in SKIP:
-            w(f"        vn_p{p}<KIND, SAVE>({state_args()}, {x_args()}, a, vo, it, pr, vm, xr, pm);")
+            w(f"        vn_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, it, pr, vm, xr, pm, ps);")
+        # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
+        w(f"        if constexpr (CNT) {{ if (it >= 1) ps.flush({cnt_slot}, it - 1); else ps.ec = 0; }}")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
         w(f"        const rsrc_t nr = make_rsrc(pn ? pn + blk * {NZ} : a.xa, pn ? nlive * {4 * NZ} : 0);")
         w("        const uint8_t* nmp = (SAVE && a.symask) ? a.symask + it * a.symask_stride : nullptr;")
@@ -531,14 +544,14 @@ def emit(S: Spec) -> str:
                 w(f"            if (KIND == NLDPC_NEURAL || bs_) {{ {' '.join(bl)} }}")
                 w(f"            else {{ for (int k = 0; k < {nw}; ++k) B{ci}[k] = 0.f; }}")
             w("        }")
-            w(f"        wr_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, it, sv, vc);")
+            w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, lds, u, a, it, sv, vc);")
             stamp(2 + 3 * ci)
             w("        __syncthreads();")
             if "cn" not in SKIP:
-                w(f"        cn_p{p}_c{ci}<KIND, SAVE>(lds, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci});")
+                w(f"        cn_p{p}_c{ci}<KIND, MODE>(lds, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps);")
             stamp(3 + 3 * ci)
             w("        __syncthreads();")
-            w(f"        rd_p{p}_c{ci}<KIND, SAVE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm);")
+            w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, ps);")
             stamp(4 + 3 * ci)
             w("        __syncthreads();")
         w("    }")
@@ -546,14 +559,15 @@ def emit(S: Spec) -> str:
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
         w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
-        w(f"    post_p{p}<KIND, SAVE>({state_args()}, {x_args()}, a, vo, a.T, lr, vm, xr, lm);")
+        w(f"    post_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, a.T, lr, vm, xr, lm, ps);")
+        w(f"    if constexpr (CNT) ps.flush({cnt_slot}, a.T - 1);")
         w("    if (a.c2v_out) {")
         for q in range(Q):
             for k, e in enumerate(S.slots[p]):
                 w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, {ref(q, k)});")
         w("    }")
         w("}")
-    w("template <int KIND, bool SAVE>")
+    w("template <int KIND, int MODE>")
     w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void kernel(FusedArgs a) {{")
     w(f"    __shared__ float lds_all[{CF * G}];")
     w("    const int t = threadIdx.x;")
@@ -572,9 +586,18 @@ def emit(S: Spec) -> str:
     w(f"    const rsrc_t cr = make_rsrc(a.c2v_out ? a.c2v_out + blk * {S.E * Z} : a.xa, nlive * {4 * S.E * Z});")
     w(f"    float* lds = lds_all + g * {CF};")
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
-    each_part("run_p{p}<KIND, SAVE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm)", indent="    ")
+    w(f"    __shared__ int cnt_all[{G * 32}];  // count-only decode: per codeword, two iterations per word")
+    w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
+    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all)", indent="    ")
+    w("    if constexpr (CNT) {")
+    w("        __syncthreads();")
+    w(f"        for (int i = t; i < nlive * a.T; i += {S.threads}) count_frame(a, cnt_all, i / a.T, i % a.T);")
+    w("    }")
     w("}")
     w("#undef D1_BYPASS")
+    w("#undef SAVE")
+    w("#undef CNT")
+    w("#undef CM")
     w("}  // namespace")
     return "\n".join(L)
 
@@ -878,11 +901,14 @@ def emit_bwd(S: Spec) -> str:
     return "\n".join(L)
 
 
+MODES = (0, 1, 2, 3)  # forward kernels: decode / decode + save for backward / count-only decode (all-zero codeword / y)
+
+
 def main():
-    """Writes OUTDIR/fused_<tag>_s<SAVE>.hip (one translation unit per base graph and SAVE variant,
+    """Writes OUTDIR/fused_<tag>_s<MODE>.hip (one translation unit per base graph and MODE variant,
     so make -j compiles them in parallel) and OUTDIR/fused_table.hip (the FusedSpec table)."""
     if sys.argv[1] == "--list":  # file names, for the Makefile
-        print(" ".join([f"fused_{t[0]}_s{v}.hip" for t in SPECS for v in (0, 1)] +
+        print(" ".join([f"fused_{t[0]}_s{v}.hip" for t in SPECS for v in MODES] +
                        [f"fused_{t[0]}_bwd.hip" for t in SPECS] + ["fused_table.hip"]))
         return
     outdir, res = sys.argv[1], sys.argv[2]
@@ -906,13 +932,13 @@ def main():
 
     for S, on in specs:
         body = emit(S) if on else ""
-        for save in (0, 1):
+        for save in MODES:
             src = list(head)
             src.append(body)
             src.append(f"void* fused_{S.tag}_kernel_s{save}(int kind) {{")
             if on:
                 for k in kinds:
-                    src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, {'true' if save else 'false'}>);")
+                    src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, {save}>);")
             src.append("    return nullptr;")
             src.append("}")
             src.append("}  // namespace nldpc")
@@ -929,19 +955,18 @@ def main():
         write(f"fused_{S.tag}_bwd.hip", src)
     src = list(head)
     for S, _ in specs:
-        src.append(f"void* fused_{S.tag}_kernel_s0(int kind);")
-        src.append(f"void* fused_{S.tag}_kernel_s1(int kind);")
+        for v in MODES:
+            src.append(f"void* fused_{S.tag}_kernel_s{v}(int kind);")
         src.append(f"void* fused_{S.tag}_bwd(int kind);")
         src.append(f"static const int32_t basegraph_{S.tag}[{S.M * S.N}] = "
                    f"{{{', '.join(str(int(x)) for x in S.hb.reshape(-1))}}};")
     src.append("const FusedSpec* fused_specs(int* n) {")
     src.append(f"    static const FusedSpec tab[{len(specs)}] = {{")
     for S, _ in specs:
-        k0 = ", ".join(f"fused_{S.tag}_kernel_s0({k})" for k in range(4))
-        k1 = ", ".join(f"fused_{S.tag}_kernel_s1({k})" for k in range(4))
+        ks = ", ".join("{" + ", ".join(f"fused_{S.tag}_kernel_s{v}({k})" for k in range(4)) + "}" for v in MODES)
         kb = ", ".join(f"fused_{S.tag}_bwd({k})" for k in range(4))
         src.append(f"        {{\"{S.tag}\", {S.M}, {S.N}, {S.Z}, {S.E}, {S.G}, {S.threads}, basegraph_{S.tag}, "
-                   f"{{{{{k0}}}, {{{k1}}}}}, {{{kb}}}, {S.lanes // 64}}},")
+                   f"{{{ks}}}, {{{kb}}}, {S.lanes // 64}}},")
     src.append("    };")
     src.append(f"    *n = {len(specs)};")
     src.append("    return tab;")

@@ -262,7 +262,8 @@ static bool fused_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T
 
 static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
                          const float* w_cn, const float* bias, const float* w_vn, float* const* outs, float* c2v,
-                         void* saved, hipStream_t s) {
+                         void* saved, hipStream_t s, const uint8_t* cnt_y = nullptr, int32_t cnt_conv = 0,
+                         int64_t* counts = nullptr) {
     int n = 0;
     const FusedSpec& f = fused_specs(&n)[g->fused];
     FusedArgs fa{};
@@ -277,7 +278,10 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     fa.lo = cfg->llr_lo;
     fa.hi = cfg->llr_hi;
     fa.c2v_out = (cfg->flags & NLDPC_FLAG_NO_STATE) ? nullptr : c2v;
-    for (int k = 0; k < kFusedMaxT; ++k) fa.outs.p[k] = k < T ? outs[k] : nullptr;
+    for (int k = 0; k < kFusedMaxT; ++k) fa.outs.p[k] = (outs && k < T) ? outs[k] : nullptr;
+    fa.cnt_y = cnt_y;
+    fa.cnt_conv = cnt_conv;
+    fa.cnt = reinterpret_cast<unsigned long long*>(counts);
     if (saved) {
         const SavedLayout SL = saved_layout(g, cfg, B, T);
         char* sb = static_cast<char*>(saved);
@@ -296,8 +300,8 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     void* args[] = {&fa};
     const int64_t blocks = (B + f.G - 1) / f.G;
     prof_start(PROF_FUSED, s);
-    hipError_t e = hipLaunchKernel(f.kernels[saved ? 1 : 0][cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args,
-                                   0, s);
+    const int mode = saved ? 1 : (counts ? (cnt_y ? 3 : 2) : 0);
+    hipError_t e = hipLaunchKernel(f.kernels[mode][cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args, 0, s);
     prof_stop(s);
     if (e == hipSuccess) e = hipGetLastError();
     if (stamp_file && e == hipSuccess) {
@@ -429,4 +433,25 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
         if (e != hipSuccess) return hip_fail(e, "posterior launch");
     }
     return NLDPC_OK;
+}
+
+extern "C" int nldpc_forward_count(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
+                                   const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
+                                   const uint8_t* y, int32_t convention, int64_t* counts, void* stream) {
+    int st = validate_cfg(g, cfg, B, T);
+    if (st) return st;
+    if (!xa || !counts) return fail(NLDPC_EINVAL, "nldpc_forward_count: xa and counts are required");
+    if (convention != 0 && convention != 1) return fail(NLDPC_EINVAL, "nldpc_forward_count: convention is 0 or 1");
+    if (cfg->kind == NLDPC_NEURAL && (!w_cn || !bias))
+        return fail(NLDPC_EINVAL, "nldpc_forward_count: the Neural decoder needs w_cn and bias");
+    if (cfg->vn_cumulative && !w_vn) return fail(NLDPC_EINVAL, "nldpc_forward_count: vn_cumulative needs w_vn");
+    (void)w_ucn;
+    if (!fused_eligible(g, cfg, T, false))
+        return fail(NLDPC_EUNSUPPORTED, "nldpc_forward_count: needs the fused path (a compiled base graph, no UCN, "
+                                        "fresh state, T <= 64); use nldpc_forward + nldpc_ber_count instead");
+    DeviceGuard guard(g->device);
+    nldpc_cfg c = *cfg;
+    c.flags |= NLDPC_FLAG_NO_STATE;
+    return fused_forward(g, &c, B, T, xa, w_cn, bias, w_vn, nullptr, nullptr, nullptr, static_cast<hipStream_t>(stream),
+                         y, convention, counts);
 }

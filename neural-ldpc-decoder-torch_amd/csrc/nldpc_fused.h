@@ -29,6 +29,10 @@ struct FusedArgs {
     float* sxin;         // [T][B][N][Z] channel value xin of every iteration (cumulative VN weights), or nullptr
     int64_t sv2c_stride, symask_stride, sxin_stride;  // elements per iteration
     OutPtrs outs;        // T posteriors [B][N][Z] (nullptr entries are skipped)
+    // count-only decode (MODE 2 kernels): nldpc_forward_count
+    const uint8_t* cnt_y;  // [B][N][Z] codeword bits (MODE 3), or nullptr (all-zero codeword, MODE 2)
+    int32_t cnt_conv;      // 0: bit = LLR > 0; 1: bit = LLR < 0
+    unsigned long long* cnt;  // [T][2] (+=) bit errors, frame errors
     uint64_t* stamps;    // diagnostic stamp build only (make STAMPS=1): [256][waves][T][8] s_memtime
 };
 
@@ -179,6 +183,42 @@ struct FusedBwdArgs {
 __device__ __forceinline__ uint32_t bload8(rsrc_t r, uint32_t vo, int so) {
     return __builtin_amdgcn_raw_buffer_load_b8(r, vo, so, 0);
 }
+// Where a posterior goes.  Decode kernels store it; count-only kernels (CNT) compare its hard decision
+// with the codeword bit and count the difference (Functions.py:85-102 evaluate_ber_fer on every
+// iteration's output, without writing the T posteriors).
+struct PostSink {
+    rsrc_t yr;  // codeword bits [N][Z] per codeword (empty descriptor: all-zero codeword)
+    int ec;     // this thread's bit errors of the iteration being completed
+    int conv;
+    // the errors of iteration `it` into this codeword's LDS counters (two iterations per word)
+    __device__ __forceinline__ void flush(int* cntl, int it) {
+        if (ec) atomicAdd(cntl + (it >> 1), ec << ((it & 1) * 16));
+        ec = 0;
+    }
+};
+// CM 0: store; 1: count against the all-zero codeword; 2: count against y (its loads cost registers
+// the decoder state needs, hence a kernel variant of its own)
+template <int CM>
+__device__ __forceinline__ void put_post(rsrc_t pr, uint32_t vo, int so, float v, PostSink& ps) {
+    if constexpr (CM == 0) {
+        bstore(pr, vo, so, v);
+    } else {
+        const uint32_t bit = ps.conv ? (v < 0.f) : (v > 0.f);
+        uint32_t y = 0u;
+        // byte offset of the bit = float offset / 4; the sum first: a rotated copy's lane offset can
+        // wrap below zero (vo + (-4Z)), which only the 32-bit total undoes
+        if constexpr (CM == 2) y = __builtin_amdgcn_raw_buffer_load_b8(ps.yr, (vo + (uint32_t)so) >> 2, 0, 0) & 1u;
+        ps.ec += (int)(bit ^ y);
+    }
+}
+// end of a count-only decode: codeword g of the workgroup, iteration it -> the global counters
+__device__ __forceinline__ void count_frame(const FusedArgs& a, const int* cnt_all, int g, int it) {
+    const unsigned v = ((unsigned)cnt_all[g * 32 + (it >> 1)] >> ((it & 1) * 16)) & 0xFFFFu;
+    if (v) {
+        atomicAdd(a.cnt + 2 * it, (unsigned long long)v);
+        atomicAdd(a.cnt + 2 * it + 1, 1ull);
+    }
+}
 // dL/dy of one variable copy through the Boosted output clamp (mask saved by the forward)
 template <int KIND>
 __device__ __forceinline__ float gy_masked(rsrc_t gr, rsrc_t mr, uint32_t vo, uint32_t vm, int so) {
@@ -276,7 +316,7 @@ struct FusedSpec {
     const char* tag;
     int32_t M, N, Z, E, G, threads;
     const int32_t* basegraph;  // [M*N]
-    void* kernels[2][4];       // [SAVE][nldpc_kind]
+    void* kernels[4][4];       // [MODE: decode / save / count / count against y][nldpc_kind]
     void* bwd[4];              // backward kernels [nldpc_kind]
     int32_t waves_per_part;    // partial-sum slots per workgroup
 };

@@ -21,7 +21,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
-from nldpc.decode import KIND_MS, KIND_QMS, KIND_SP, DecodeCfg, decode_autograd
+from nldpc.decode import KIND_MS, KIND_QMS, KIND_SP, DecodeCfg, decode_autograd, decode_count
 
 from boosted_neural_ldpc_decoder.ConnectingMatrixTorch import ConnectingMatrixTorch
 from boosted_neural_ldpc_decoder.Functions import Functions
@@ -229,6 +229,23 @@ class BoostedNeuralLDPCDecoder(nn.Module):
         if ucn > 0 and ucn == cn and cn in (1, 2, 3):
             w_ucn = self._per_edge(self.fetch_param(ParamType.Weight, NodeType.UCN, it), cn, "UCN")
         return w_cn, w_ucn, w_vn
+
+    @torch.no_grad()
+    def count_errors(self, xa, y=None, convention=0):
+        """Count-only decode (extension): int64 [T, 2] device tensor of (bit errors, frame
+        errors) of iterations 0..T-1 of forward(xa) (target_iter None, no fixed iterations), as
+        nldpc.channel.ber_counts(outputs, y, convention=...) would count them, without writing the
+        posteriors (nor self.outputs / self.llr).  y: [B, N*Z] codeword bits or None (all-zero)."""
+        T = self.iter_node_counts
+        ws = [self._iteration_weights(it, [], None, 0, xa.device) for it in range(T)]
+        stack = lambda k: torch.stack([w[k] for w in ws]) if ws[0][k] is not None else None  # noqa: E731
+        w_cn, w_ucn, w_vn = stack(0), stack(1), stack(2)
+        qbit = self.decoder_qms_qbit if self.decoding_type == DecoderType.QMS else 0
+        cfg = DecodeCfg(kind=_KIND[self.decoding_type], qbit=qbit, ucn=w_ucn is not None,
+                        vn_cumulative=w_vn is not None, llr_lo=float(self.allowed_llr_range.start),
+                        llr_hi=float(self.allowed_llr_range.end), keep_state=False)
+        return decode_count(self.conn_mat.graph, cfg, xa, T, w_cn=w_cn, w_ucn=w_ucn, w_vn=w_vn, y=y,
+                            convention=convention)
 
     # ------------------------------------------------------------------ forward
     def forward(self, xa, target_iter=None, fixed_iter=None, fixed_iter_weight=None):

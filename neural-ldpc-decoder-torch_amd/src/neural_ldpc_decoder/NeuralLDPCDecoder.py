@@ -10,7 +10,7 @@ registered (22.9 GB each at z=384); their keys in an old state_dict are accepted
 import torch
 import torch.nn as nn
 
-from nldpc.decode import KIND_NEURAL, DecodeCfg, decode_autograd
+from nldpc.decode import KIND_NEURAL, DecodeCfg, decode_autograd, decode_count
 
 from .ConnectingMatrixTorch import ConnectingMatrixTorch
 
@@ -49,3 +49,13 @@ class NeuralLDPCDecoder(nn.Module):
         b = torch.stack(list(self.biases_var))
         outs, _ = decode_autograd(self.conn_mat.graph, self._cfg, xa, T, w_cn=w, bias=b)
         return outs
+
+    @torch.no_grad()
+    def count_errors(self, xa, y=None, convention=0):
+        """Count-only decode (extension): int64 [T, 2] device tensor of (bit errors, frame
+        errors) per iteration, equal to nldpc.channel.ber_counts(self.forward(xa), y, convention=...)
+        without materialising the T posteriors.  y: [B, N*Z] codeword bits or None (all-zero)."""
+        T = self.iter_node_counts
+        w = torch.stack(list(self.weights_var))
+        b = torch.stack(list(self.biases_var))
+        return decode_count(self.conn_mat.graph, self._cfg, xa, T, w_cn=w, bias=b, y=y, convention=convention)

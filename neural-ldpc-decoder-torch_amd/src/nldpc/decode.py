@@ -97,6 +97,38 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
     return outs, state, saved
 
 
+def decode_count(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn=None, w_ucn=None, bias=None,
+                 w_vn=None, y=None, convention: int = 0) -> torch.Tensor:
+    """Count-only decode: int64 [T, 2] device tensor of (bit errors, frame errors) of
+    every iteration's posterior -- what decode(...) followed by channel.ber_counts(outputs, y,
+    convention=...) returns, counted inside the fused kernel (nldpc_forward_count) so the T posteriors
+    are never written.  Configurations the fused path does not cover (UCN, a resumed state, a graph
+    without a compiled kernel) run decode + the device counter instead (both on the device)."""
+    _require_device_tensor(xa, "xa")
+    if xa.dim() != 3 or xa.shape[1] != graph.N or xa.shape[2] != graph.Z:
+        raise ValueError(f"xa must be [B, {graph.N}, {graph.Z}], got {tuple(xa.shape)}")
+    dev = xa.device
+    B = int(xa.shape[0])
+    c = cfg.c_struct(False)
+    c.flags |= _lib.FLAG_NO_STATE
+    L = _lib.lib()
+    h = graph.handle(dev)
+    fast = ctypes.c_int32(0)
+    _lib.check(L.nldpc_fast_path(h, ctypes.byref(c), B, T, 0, ctypes.byref(fast)), "nldpc_fast_path")
+    yb = None if y is None else (y != 0).to(torch.uint8).reshape(B, graph.N * graph.Z).contiguous()
+    if not fast.value:
+        from .channel import ber_counts
+        outs, _, _ = decode(graph, cfg, xa, T, w_cn=w_cn, w_ucn=w_ucn, bias=bias, w_vn=w_vn)
+        return ber_counts(list(outs), yb, convention=convention)
+    counts = torch.zeros((T, 2), dtype=torch.int64, device=dev)
+    xa_c = _f32c(xa)
+    w_cn, w_ucn, bias, w_vn = _f32c(w_cn), _f32c(w_ucn), _f32c(bias), _f32c(w_vn)
+    _lib.check(L.nldpc_forward_count(h, ctypes.byref(c), B, T, _lib.ptr(xa_c), _lib.ptr(w_cn), _lib.ptr(w_ucn),
+                                     _lib.ptr(bias), _lib.ptr(w_vn), _lib.ptr(yb), int(convention),
+                                     counts.data_ptr(), _lib.stream_of(dev)), "nldpc_forward_count")
+    return counts
+
+
 def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, saved, *, w_cn=None, w_ucn=None,
                     bias=None, w_vn=None, app_prev=None, need=(True, True, True, True)):
     """Gradients of the per-edge / per-column weights.  Returns (g_w_cn, g_w_ucn, g_bias, g_w_vn)."""

@@ -223,3 +223,48 @@ def test_fused_backward_equals_stream(kind, Z, B):
             np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-5 * max(np.abs(a).max(), 1e-12))
             n += 1
     assert n == 2
+
+
+@pytest.mark.parametrize("bg,Z,B", [("bg2", 384, 5), ("bg2", 16, 37), ("wimax", 24, 23)])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_count_only_decode_equals_decode_then_count(bg, Z, B, kind):
+    """§8 F2: the fused count-only kernels (nldpc_forward_count) give exactly the per-iteration
+    (bit errors, frame errors) of decode + ber_counts, against the all-zero codeword and against a
+    given y, in both decision conventions (partial last workgroup included: B % G != 0)."""
+    from nldpc.channel import ber_counts
+    from nldpc.decode import KIND_NEURAL, DecodeCfg, decode, decode_count
+    g = _graph(BG2 if bg == "bg2" else WIMAX, Z)
+    T = 7
+    gen = torch.Generator().manual_seed(100 * kind + Z)
+    x = (2 * (-1 + 1.1 * torch.randn(B, g.N, Z, generator=gen)) / 1.21).float().to(DEV)
+    if kind == KIND_NEURAL:
+        kw = dict(w_cn=(torch.rand(T, g.E, generator=gen) * 1.2).to(DEV),
+                  bias=(torch.randn(T, g.E, generator=gen) * 0.1).to(DEV))
+    else:
+        kw = dict(w_cn=(0.5 + torch.rand(T, g.M, generator=gen))[:, torch.as_tensor(g.chk)].contiguous().to(DEV),
+                  w_vn=(0.8 + 0.4 * torch.rand(T, g.N, generator=gen)).to(DEV))
+    cfg = DecodeCfg(kind=kind, qbit=5, vn_cumulative=kind != KIND_NEURAL, keep_state=False)
+    outs, _, _ = decode(g, cfg, x, T, **kw)
+    ys = [None, torch.randint(0, 2, (B, g.N * Z), generator=gen).to(DEV),
+          torch.ones((B, g.N * Z), dtype=torch.uint8, device=DEV)]
+    for y in ys:
+        for conv in (0, 1):
+            ref = ber_counts(list(outs), y, convention=conv)
+            got = decode_count(g, cfg, x, T, y=y, convention=conv, **kw)
+            assert torch.equal(got, ref), (y is None, conv, got.cpu().tolist(), ref.cpu().tolist())
+    fast = DecodeCfg(kind=kind, qbit=5, vn_cumulative=kind != KIND_NEURAL, path="fused")
+    decode(g, fast, x, 1, **{k: v[:1] for k, v in kw.items()})  # this configuration is on the fused path
+
+
+def test_count_only_decode_ucn_falls_back():
+    """Configurations outside the fused path (UCN) are counted by decode + the device counter."""
+    from nldpc.channel import ber_counts
+    from nldpc.decode import KIND_MS, DecodeCfg, decode, decode_count
+    g = _graph(BG2, 16)
+    T, B = 4, 9
+    gen = torch.Generator().manual_seed(5)
+    x = (2 * (-1 + 1.1 * torch.randn(B, g.N, 16, generator=gen)) / 1.21).float().to(DEV)
+    w = (0.5 + torch.rand(T, g.E, generator=gen)).to(DEV)
+    cfg = DecodeCfg(kind=KIND_MS, ucn=True)
+    outs, _, _ = decode(g, cfg, x, T, w_cn=w, w_ucn=w * 0.5)
+    assert torch.equal(decode_count(g, cfg, x, T, w_cn=w, w_ucn=w * 0.5), ber_counts(list(outs)))

@@ -100,6 +100,10 @@ def test_boosted_module_forward(golden, name):
             assert outs is model.outputs  # module-owned list, as in the reference
     for t, o in enumerate(outs):
         _assert_out(o, d["outputs"][t], int(d["dtype"]) == 0)
+    if "target6" not in name and not d.get("fixed_nodes", np.zeros(0)).size:
+        # count-only decode (§8 F2): the counts of the outputs just checked, without writing them
+        from nldpc.channel import ber_counts
+        assert torch.equal(model.count_errors(x, convention=1), ber_counts(outs, convention=1))
 
 
 TRAIN = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "train_*.npz")))

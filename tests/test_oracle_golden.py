@@ -1,9 +1,10 @@
 """Pin the CPU oracle (oracle/ldpc_oracle.py) against the reference's own outputs.
 
 The fixtures under tests/golden/ were produced by tests/golden/gen_golden.py, which runs the
-reference (ShapeLayer/neural-ldpc-decoder-torch) in the development container.  Neural / MS / QMS
-soft outputs must match bit for bit; SP within tolerance (torch.prod order)
-with identical hard decisions; gradients within rtol 1e-4 (SP: 2e-3).
+reference (ShapeLayer/neural-ldpc-decoder-torch) in the development container.  Soft outputs of
+every kind (Neural / MS / QMS / SP) must match bit for bit -- SP through the oracle's restatement of
+ATen's CPU torch.prod order (oracle/ldpc_oracle.py _prod_aten); gradients within
+rtol 1e-4 (batch-sum order).
 """
 import glob
 import os
@@ -82,11 +83,7 @@ def test_oracle_boosted(golden, name):
                            w_vn=_fetch(d, "VN", nw[2], fixed))
     o = torch.stack([outs[i] for i in iters]).numpy()
     ref = d["outputs"]
-    assert np.array_equal(o > 0, ref > 0)
-    if int(d["dtype"]) == 0:  # SP: torch.prod order is not modelled
-        np.testing.assert_allclose(o, ref, rtol=1e-3, atol=5e-3)
-    else:
-        assert np.array_equal(o, ref), f"{(o != ref).sum()} soft values differ"
+    assert np.array_equal(o, ref), f"{(o != ref).sum()} soft values differ"
 
 
 @pytest.mark.parametrize("name", ["neural_bg2_z16_b16_t5_random", "neural_wimax_z24_b16_t20_random"])
@@ -119,7 +116,7 @@ def test_oracle_boosted_grads(golden, name):
     y = torch.from_numpy(d["y"].astype(np.float32))
     loss = sum(torch.nn.functional.binary_cross_entropy_with_logits(outs[t], y) for t in range(T)) / T
     loss.backward()
-    tol = 2e-3 if int(d["dtype"]) == 0 else 1e-4
+    tol = 1e-4
     for k, p in P.items():
         if "grad__" + k in d:
             r = d["grad__" + k]
@@ -158,3 +155,16 @@ def test_oracle_reproduces_reference_ber_curve(golden):
         wrong = [(o.numpy() > 0) != y for o in outs]
         assert [int(m.sum()) for m in wrong] == d["bit_errors"][k].tolist()
         assert [int(m.any(axis=1).sum()) for m in wrong] == d["frame_errors"][k].tolist()
+
+
+@pytest.mark.parametrize("E", [7, 32, 197, 316])
+def test_prod_order_model_matches_torch_prod(E):
+    """_prod_aten's model of ATen's CPU reduction order reproduces torch.prod bit for bit on the CPU
+    the fixtures were made on (it is the order the SP fixtures above pin)."""
+    from oracle.ldpc_oracle import _prod_aten
+    gen = torch.Generator().manual_seed(E)
+    t = (torch.rand(4, 1, 64, E, generator=gen) * 1.6 - 0.8)
+    t = torch.where(torch.rand(t.shape, generator=gen) < 0.3, torch.ones_like(t), t)
+    ref = torch.prod(t, dim=3)
+    got = _prod_aten(t, list(range(E)), E)
+    assert torch.equal(got, ref), f"{(got != ref).sum().item()} of {ref.numel()} products differ"
