@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel timing")
     ap.add_argument("--no-sweep", action="store_true", help="skip the Eb/N0 1..4 dB BER sweep")
+    ap.add_argument("--no-count-only", action="store_true", help="skip the count-only decode timing (F2)")
     return ap.parse_args()
 
 
@@ -208,12 +209,28 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
         elapsed, prof = timed(args, local, dev, step, Prof(not args.no_profile, args.steps * (2 * T + 2)))
         counts = ber_counts(state["outs"])  # BER / FER per iteration, decoder convention bit = LLR > 0
         state.clear()
+        # count-only decode: the same decode with the counting fused into the kernel and
+        # no posteriors written -- reported beside the headline, never as `value`
+        count_only = None
+        if not args.no_count_only:
+            cnt = {}
+
+            def cstep():
+                cnt["c"] = model.count_errors(xa)
+
+            c_elapsed, cprof = timed(args, local, dev, cstep, Prof(not args.no_profile, args.steps + 2))
+            c_elapsed = nd_dist.max_time(c_elapsed, device=dev)
+            count_only = {"value": round(world * B * args.steps / c_elapsed, 1), "unit": "codewords/s",
+                          "ms_per_step": round(1000.0 * c_elapsed / args.steps, 3),
+                          "kernel_avg_ms": (round(cprof["fused"][0] / cprof["fused"][1], 4)
+                                            if cprof and cprof["fused"][1] else None),
+                          "counts_equal_decode_then_count": bool(torch.equal(cnt["c"], counts))}
         sweep = None
         if args.workload == "cfg3" and not args.no_sweep:
             sweep = {"ebn0_db": [], "bit_errors": [], "frame_errors": []}
             for eb in np.arange(1.0, 4.01, 0.5):
                 x = awgn_llr(B, N, Z, sigma_for(float(eb), rate), seed=2042, b_offset=offset, device=dev)
-                c = nd_dist.sum_counts(ber_counts(model(x))).cpu().numpy()
+                c = nd_dist.sum_counts(model.count_errors(x)).cpu().numpy()  # fused counting (F2)
                 sweep["ebn0_db"].append(float(eb))
                 sweep["bit_errors"].append(int(c[-1, 0]))
                 sweep["frame_errors"].append(int(c[-1, 1]))
@@ -247,6 +264,8 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
                 "bit_errors_last_iter": int(counts[-1, 0]), "bits": bits_total,
                 "ber_per_iter": [float(c) / bits_total for c in counts[:, 0]]},
     }
+    if count_only is not None:
+        res["count_only"] = count_only
     if sweep is not None:
         sweep["ber"] = [b / bits_total for b in sweep["bit_errors"]]
         sweep["fer"] = [f / (world * B) for f in sweep["frame_errors"]]

@@ -111,8 +111,8 @@ def emit(S: Spec) -> str:
     w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E};")
     w("// degree-1 edges bypass LDS (Neural inference; see the check-node section)")
     # MODE 0: decode, MODE 1: decode and save what the backward needs, MODE 2 / 3: count-only decode
-    # (the posteriors are compared with the all-zero codeword / the codeword y and counted instead of
-    # stored)
+    # (the posteriors are compared with the codeword and counted instead of stored):
+    # 2 = all-zero codeword, decoder convention; 3 = either convention, against y when given
     w("#define SAVE (MODE == 1)")
     w("#define CNT (MODE >= 2)")
     w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
@@ -423,6 +423,7 @@ def emit(S: Spec) -> str:
     # barrier counts waves, not program counters, and every part executes the same barrier sequence.
     # this thread's codeword counters (recomputed at each flush: no register held across the iteration)
     cnt_slot = "cntl" if G == 1 else f"cntl + (int)((threadIdx.x % {S.lanes}) / {ZT}) * 32"
+    cnt_flush = "flush_wave" if G == 1 else "flush"  # one codeword per wave: reduce the wave first
     for p in range(S.P):
         if PARTS and p not in PARTS:
             continue
@@ -511,7 +512,7 @@ def emit(S: Spec) -> str:
         if "vn" not in SKIP:
             w(f"        vn_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, it, pr, vm, xr, pm, ps);")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
-        w(f"        if constexpr (CNT) {{ if (it >= 1) ps.flush({cnt_slot}, it - 1); else ps.ec = 0; }}")
+        w(f"        if constexpr (CNT) {{ if (it >= 1) ps.{cnt_flush}({cnt_slot}, it - 1); else ps.ec = 0; }}")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
         w(f"        const rsrc_t nr = make_rsrc(pn ? pn + blk * {NZ} : a.xa, pn ? nlive * {4 * NZ} : 0);")
         w("        const uint8_t* nmp = (SAVE && a.symask) ? a.symask + it * a.symask_stride : nullptr;")
@@ -560,7 +561,7 @@ def emit(S: Spec) -> str:
         w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
         w(f"    post_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, a.T, lr, vm, xr, lm, ps);")
-        w(f"    if constexpr (CNT) ps.flush({cnt_slot}, a.T - 1);")
+        w(f"    if constexpr (CNT) ps.{cnt_flush}({cnt_slot}, a.T - 1);")
         w("    if (a.c2v_out) {")
         for q in range(Q):
             for k, e in enumerate(S.slots[p]):
@@ -591,7 +592,7 @@ def emit(S: Spec) -> str:
     each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all)", indent="    ")
     w("    if constexpr (CNT) {")
     w("        __syncthreads();")
-    w(f"        for (int i = t; i < nlive * a.T; i += {S.threads}) count_frame(a, cnt_all, i / a.T, i % a.T);")
+    w("        if (t < a.T) count_iteration(a, cnt_all, nlive, t);")
     w("    }")
     w("}")
     w("#undef D1_BYPASS")
@@ -901,7 +902,7 @@ def emit_bwd(S: Spec) -> str:
     return "\n".join(L)
 
 
-MODES = (0, 1, 2, 3)  # forward kernels: decode / decode + save for backward / count-only decode (all-zero codeword / y)
+MODES = (0, 1, 2, 3)  # forward kernels: decode / decode + save for backward / count-only (all-zero, LLR > 0) / count-only (general)
 
 
 def main():

@@ -300,7 +300,7 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     void* args[] = {&fa};
     const int64_t blocks = (B + f.G - 1) / f.G;
     prof_start(PROF_FUSED, s);
-    const int mode = saved ? 1 : (counts ? (cnt_y ? 3 : 2) : 0);
+    const int mode = saved ? 1 : (counts ? ((cnt_y || cnt_conv) ? 3 : 2) : 0);
     hipError_t e = hipLaunchKernel(f.kernels[mode][cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args, 0, s);
     prof_stop(s);
     if (e == hipSuccess) e = hipGetLastError();

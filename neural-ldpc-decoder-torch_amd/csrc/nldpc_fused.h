@@ -195,13 +195,18 @@ struct PostSink {
         if (ec) atomicAdd(cntl + (it >> 1), ec << ((it & 1) * 16));
         ec = 0;
     }
+    // same, when the whole wave belongs to one codeword: one LDS atomic per wave
+    __device__ __forceinline__ void flush_wave(int* cntl, int it);
 };
-// CM 0: store; 1: count against the all-zero codeword; 2: count against y (its loads cost registers
-// the decoder state needs, hence a kernel variant of its own)
+// CM 0: store; 1: count against the all-zero codeword in the decoder convention (bit = LLR > 0: one
+// compare and one add-with-carry per posterior, the BER-sweep case); 2: any convention, against y
+// when given (its loads cost registers the decoder state needs, hence a kernel variant of its own)
 template <int CM>
 __device__ __forceinline__ void put_post(rsrc_t pr, uint32_t vo, int so, float v, PostSink& ps) {
     if constexpr (CM == 0) {
         bstore(pr, vo, so, v);
+    } else if constexpr (CM == 1) {
+        ps.ec += v > 0.f ? 1 : 0;
     } else {
         const uint32_t bit = ps.conv ? (v < 0.f) : (v > 0.f);
         uint32_t y = 0u;
@@ -211,12 +216,18 @@ __device__ __forceinline__ void put_post(rsrc_t pr, uint32_t vo, int so, float v
         ps.ec += (int)(bit ^ y);
     }
 }
-// end of a count-only decode: codeword g of the workgroup, iteration it -> the global counters
-__device__ __forceinline__ void count_frame(const FusedArgs& a, const int* cnt_all, int g, int it) {
-    const unsigned v = ((unsigned)cnt_all[g * 32 + (it >> 1)] >> ((it & 1) * 16)) & 0xFFFFu;
-    if (v) {
-        atomicAdd(a.cnt + 2 * it, (unsigned long long)v);
-        atomicAdd(a.cnt + 2 * it + 1, 1ull);
+// end of a count-only decode: iteration it of the workgroup's nlive codewords -> the global counters
+// (summed over the workgroup first: two global atomics per iteration and workgroup)
+__device__ __forceinline__ void count_iteration(const FusedArgs& a, const int* cnt_all, int nlive, int it) {
+    unsigned long long bits = 0, frames = 0;
+    for (int g = 0; g < nlive; ++g) {
+        const unsigned v = ((unsigned)cnt_all[g * 32 + (it >> 1)] >> ((it & 1) * 16)) & 0xFFFFu;
+        bits += v;
+        frames += v != 0;
+    }
+    if (bits) {
+        atomicAdd(a.cnt + 2 * it, bits);
+        atomicAdd(a.cnt + 2 * it + 1, frames);
     }
 }
 // dL/dy of one variable copy through the Boosted output clamp (mask saved by the forward)
@@ -242,6 +253,11 @@ __device__ __forceinline__ float wave_sum(float x) {
     x += dpp_mov<0x142, 0xa>(x);  // row_bcast:15 into rows 1, 3: rows 0+1 | 2+3
     x += dpp_mov<0x143, 0xc>(x);  // row_bcast:31 into rows 2, 3: lane 63 = the wave's sum
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
+}
+__device__ __forceinline__ void PostSink::flush_wave(int* cntl, int it) {
+    const int s = (int)wave_sum((float)ec);  // exact: counts below 2^24
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(cntl + (it >> 1), s << ((it & 1) * 16));
+    ec = 0;
 }
 
 // Boosted MS / QMS (active quantiser) check node of one check copy in place, specialised like

@@ -1,6 +1,7 @@
 """GPU parity of the forward decode (HIP kernels through the C ABI) against the reference's golden
 outputs and the CPU oracle.  Neural / MS / QMS: bit-exact soft outputs; SP: hard decisions exact,
-soft values within rtol 1e-3 / atol 5e-3 (torch.prod order + device tanh/atanh ulps).
+soft values within rtol 1e-3 / atol 5e-3 and at most 0.1 % of them beyond 1e-4 relative (device
+tanh/atanh ulps and product order, amplified by atanh near saturation).
 """
 import glob
 import os
@@ -16,6 +17,15 @@ pytestmark = pytest.mark.gpu
 BG2 = np.loadtxt(os.path.join(ROOT, "resources", "basegraph2_set0.txt"), int, delimiter="\t")
 WIMAX = np.loadtxt(os.path.join(ROOT, "resources", "wman_N0576_R34_z24.txt"), int, delimiter="\t")
 DEV = torch.device("cuda")
+
+
+def sp_rel_outliers(o, ref):
+    """Fraction of SP soft values beyond the north-star 1e-4 relative agreement.  The oracle reproduces
+    the reference bit for bit (torch.prod order, tests/test_oracle_golden.py); the device differs by
+    the ulps of tanhf/atanhf (vs ATen's SLEEF / glibc) and its product order, which atanh amplifies
+    by 1/(1-P^2) near saturation: measured 0-23 of 33280 values (<= 0.07 %), DESIGN.md §6."""
+    rel = np.abs(o - ref) / np.maximum(np.abs(ref), 1e-30)
+    return float((rel > 1e-4).mean())
 
 
 def _bg(name):
@@ -99,6 +109,7 @@ def test_boosted_forward_matches_reference(golden, name, path):
     assert np.array_equal(o > 0, ref > 0)
     if kind == 0:
         np.testing.assert_allclose(o, ref, rtol=1e-3, atol=5e-3)
+        assert sp_rel_outliers(o, ref) <= 1e-3
     else:
         assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} soft values differ"
 

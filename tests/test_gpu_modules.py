@@ -53,6 +53,10 @@ def _assert_out(o, ref, sp):
     assert np.array_equal(o > 0, ref > 0)
     if sp:
         np.testing.assert_allclose(o, ref, rtol=1e-3, atol=5e-3)
+        rel = np.abs(o - ref) / np.maximum(np.abs(ref), 1e-30)
+        # as test_gpu_forward.sp_rel_outliers (<= 0.1 % over a whole decode), here per single iteration's
+        # [B, N*Z] output, where a handful of saturated values is already 0.1-0.3 %
+        assert (rel > 1e-4).mean() <= 1e-2
     else:
         assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} soft values differ"
 
