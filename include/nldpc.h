@@ -179,6 +179,16 @@ int nldpc_bce_grad(const float* const* logits, int32_t K, const float* coef, con
  *   qbit != 0 applies the QMS quantiser (Functions.Cal_MSA_Q, Functions.py:69-83). */
 int nldpc_awgn_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,
                    int32_t qbit, void* stream);
+/* ---- the same channel with the rest of AWGNPassedDatagen._gendata_* (AWGNPassedDatagen.py:75-134,
+ *      §8 F1): y [B][L] uint8 codeword bits (NULL = all-zero), BPSK (-1)^(1-y); after the quantiser,
+ *      bits [puncture_start-1, puncture_end) of every codeword are set to puncture_value (the
+ *      reference: 0, or 0.001 for SP) and bits [shorten_start-1, shorten_end) to shorten_value
+ *      (-|allowed_llr_range.end|); a start of 0 disables the range (Puncture(0, 0) / Shortening(0, 0)).
+ *      nldpc_awgn_llr(...) == nldpc_channel_llr(..., NULL, 0, 0, 0, 0, 0, 0, stream). */
+int nldpc_channel_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,
+                      int32_t qbit, const uint8_t* y, int64_t puncture_start, int64_t puncture_end,
+                      float puncture_value, int64_t shorten_start, int64_t shorten_end, float shorten_value,
+                      void* stream);
 
 /* ---- benchmark instrumentation: per-kernel HIP-event timing of nldpc_forward / nldpc_backward
  *   launches.  nldpc_profile_begin arms a recorder for up to `capacity` launches (not thread-safe);

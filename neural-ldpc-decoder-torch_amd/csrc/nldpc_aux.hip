@@ -31,8 +31,17 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 __device__ __forceinline__ double u01(uint32_t r) { return ((double)r + 1.0) * (1.0 / 4294967296.0); }
 
 // one thread = 4 consecutive elements of the global (b_offset + b) * L + n stream
+// Channel options beyond the all-zero codeword (F1; AWGNPassedDatagen.py:75-134): the codeword bits y
+// (BPSK (-1)^(1-y)), and the punctured / shortened bit ranges [start-1, end) of every codeword set to a
+// constant after the quantiser (the reference's order).  start = 0: no range.
+struct ChannelOpts {
+    const uint8_t* y;  // [B][L] or nullptr
+    int64_t L, p0, p1, s0, s1;
+    float pval, sval;
+};
+
 __global__ __launch_bounds__(256) void awgn_kernel(float* xa, int64_t total, int64_t first, double sigma,
-                                                   uint64_t seed, int qbit) {
+                                                   uint64_t seed, int qbit, ChannelOpts o) {
     const int64_t g4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // local group of 4
     const int64_t g0 = (first >> 2) + g4;                                 // global group index
     const int64_t e0 = g0 * 4;
@@ -46,10 +55,15 @@ __global__ __launch_bounds__(256) void awgn_kernel(float* xa, int64_t total, int
     for (int q = 0; q < 4; ++q) {
         const int64_t e = e0 + q;
         if (e < first || e >= first + total) continue;
-        // all-zero codeword: BPSK bit 0 -> -1 (AWGNPassedDatagen.py:97-103), LLR = 2 y / sigma^2
-        float llr = (float)(2.0 * (-1.0 + sigma * n[q]) / s2);
+        // BPSK bit 0 -> -1, 1 -> +1 (AWGNPassedDatagen.py:97-103), LLR = 2 y / sigma^2
+        const int64_t i = e - first;
+        const double bpsk = (o.y && o.y[i]) ? 1.0 : -1.0;
+        float llr = (float)(2.0 * (bpsk + sigma * n[q]) / s2);
         if (qbit) llr = quantize(llr, qbit);
-        xa[e - first] = llr;
+        const int64_t k = i % o.L;  // bit index within the codeword
+        if (k >= o.p0 && k < o.p1) llr = o.pval;
+        if (k >= o.s0 && k < o.s1) llr = o.sval;
+        xa[i] = llr;
     }
 }
 
@@ -201,14 +215,26 @@ extern "C" int nldpc_bce_grad(const float* const* logits, int32_t K, const float
 
 extern "C" int nldpc_awgn_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,
                               int32_t qbit, void* stream) {
-    if (!xa || B <= 0 || L <= 0 || !(sigma > 0.f)) return fail(NLDPC_EINVAL, "nldpc_awgn_llr: bad argument");
+    return nldpc_channel_llr(xa, B, L, sigma, seed, b_offset, qbit, nullptr, 0, 0, 0.f, 0, 0, 0.f, stream);
+}
+
+extern "C" int nldpc_channel_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,
+                                 int32_t qbit, const uint8_t* y, int64_t puncture_start, int64_t puncture_end,
+                                 float puncture_value, int64_t shorten_start, int64_t shorten_end, float shorten_value,
+                                 void* stream) {
+    if (!xa || B <= 0 || L <= 0 || !(sigma > 0.f)) return fail(NLDPC_EINVAL, "nldpc_channel_llr: bad argument");
+    if (puncture_start < 0 || shorten_start < 0 || puncture_end > L || shorten_end > L)
+        return fail(NLDPC_EINVAL, "nldpc_channel_llr: puncture / shortening range outside the codeword");
+    ChannelOpts o{y, L, 0, 0, 0, 0, puncture_value, shorten_value};
+    if (puncture_start > 0) { o.p0 = puncture_start - 1; o.p1 = puncture_end; }
+    if (shorten_start > 0) { o.s0 = shorten_start - 1; o.s1 = shorten_end; }
     const int64_t total = B * L;
     const int64_t first = b_offset * L;
     const int64_t groups = ((first + total + 3) >> 2) - (first >> 2);
     const int64_t blocks = (groups + 255) / 256;
     if (blocks > 0x7FFFFFFF) return fail(NLDPC_EUNSUPPORTED, "nldpc_awgn_llr: too large");
     hipLaunchKernelGGL(awgn_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), xa, total,
-                       first, (double)sigma, seed, qbit);
+                       first, (double)sigma, seed, qbit, o);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? NLDPC_OK : hip_fail(e, "awgn_kernel launch");
 }

@@ -1,6 +1,7 @@
 """On-device channel model and error accounting (the steps either side of the decode path).
 
-awgn_llr       all-zero codeword over BPSK/AWGN, LLR = 2*(-1 + sigma*n)/sigma^2, n from Philox-4x32-10 at
+awgn_llr       codeword (all-zero or given y) over BPSK/AWGN, LLR = 2*((-1)^(1-y) + sigma*n)/sigma^2, with the
+               reference's QMS quantiser, puncturing and shortening; n from Philox-4x32-10 at
                counter (b_offset + b)*L + k: a batch sharded over ranks draws exactly the noise of the
                unsharded batch (replaces the numpy per-codeword loop of AWGNPassedDatagen.py:75-193).
 sigma_for      the reference's Eb/N0 -> sigma mapping with its code-rate formula (AWGNPassedDatagen.py:47-49).
@@ -26,13 +27,27 @@ def boosted_code_rate(N: int, M: int, n_punct: int = 1, n_short: int = 1) -> flo
 
 
 def awgn_llr(B: int, N: int, Z: int, sigma: float, *, seed: int = 2042, b_offset: int = 0, qbit: int = 0,
-             device=None, out: torch.Tensor | None = None) -> torch.Tensor:
+             device=None, out: torch.Tensor | None = None, y: torch.Tensor | None = None, puncturing=None,
+             shortening=None, puncture_value: float = 0.0, shortening_value: float = -20.0) -> torch.Tensor:
+    """[B, N, Z] fp32 channel LLRs on the device.  y: [B, N*Z] codeword bits (None = all-zero);
+    puncturing / shortening: (start, end) 1-based inclusive bit ranges of every codeword, or objects
+    with .start / .end (the reference's Puncture / Shortening; start 0 = none), set after the QMS
+    quantiser to puncture_value (reference: 0, 0.001 for SP) / shortening_value (-|llr_hi|)."""
     device = torch.device(device if device is not None else "cuda")
     if out is None:
         out = torch.empty((B, N, Z), dtype=torch.float32, device=device)
     L = N * Z
-    _lib.check(_lib.lib().nldpc_awgn_llr(out.data_ptr(), B, L, float(sigma), int(seed) & (2 ** 64 - 1), int(b_offset),
-                                         int(qbit), _lib.stream_of(out.device)), "nldpc_awgn_llr")
+    rng = lambda r: (0, 0) if r is None else ((r.start, r.end) if hasattr(r, "start") else tuple(r))  # noqa: E731
+    (p0, p1), (s0, s1) = rng(puncturing), rng(shortening)
+    yb = None
+    if y is not None:
+        if y.device != out.device or y.numel() != B * L:
+            raise ValueError(f"y must be a [B, N*Z] = [{B}, {L}] tensor on {out.device}")
+        yb = (y != 0).to(torch.uint8).reshape(B, L).contiguous()
+    _lib.check(_lib.lib().nldpc_channel_llr(out.data_ptr(), B, L, float(sigma), int(seed) & (2 ** 64 - 1),
+                                            int(b_offset), int(qbit), _lib.ptr(yb), int(p0), int(p1),
+                                            float(puncture_value), int(s0), int(s1), float(shortening_value),
+                                            _lib.stream_of(out.device)), "nldpc_channel_llr")
     return out
 
 

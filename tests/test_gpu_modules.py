@@ -176,6 +176,38 @@ def test_awgn_llr_statistics_and_sharding():
     assert not torch.equal(full, other)
 
 
+@pytest.mark.parametrize("qbit", [0, 5])
+def test_channel_codeword_puncture_shorten(qbit):
+    """§8 F1 on the device: given codeword bits (BPSK (-1)^(1-y)), the QMS quantiser, then puncturing /
+    shortening of 1-based inclusive bit ranges -- the steps of AWGNPassedDatagen._generate
+    (AWGNPassedDatagen.py:75-134), here over the device's Philox noise (the reference's numpy stream is
+    pinned by the host restatement, tests/test_api_surface.py)."""
+    from boosted_neural_ldpc_decoder.Functions import Functions
+    from boosted_neural_ldpc_decoder.struct.Puncture import Puncture
+    from nldpc.channel import awgn_llr
+    B, N, Z, sigma = 24, 52, 16, 0.7
+    L = N * Z
+    gen = torch.Generator().manual_seed(qbit)
+    y = torch.randint(0, 2, (B, L), generator=gen).to(DEV)
+    plain = awgn_llr(B, N, Z, sigma, seed=5, b_offset=3, device=DEV)  # all-zero codeword, no quantiser
+    noise = (plain.double().reshape(B, L) * sigma ** 2 / 2 + 1) / sigma
+    want = 2 * ((2 * y.double() - 1) + sigma * noise) / sigma ** 2
+    if qbit:
+        want = torch.as_tensor(Functions.Cal_MSA_Q(want.float().cpu().numpy(), qbit), device=DEV).double()
+    want[:, 0:2 * Z] = 0.001          # Puncture(1, 2Z): columns 0 and 1
+    want[:, 100:130] = -20.0          # Shortening(101, 130)
+    got = awgn_llr(B, N, Z, sigma, seed=5, b_offset=3, qbit=qbit, device=DEV, y=y, puncturing=Puncture(1, 2 * Z),
+                   shortening=(101, 130), puncture_value=0.001, shortening_value=-20.0).reshape(B, L)
+    if qbit:  # on the quantiser's grid: equal except where the rounding of the recovered noise flips a step
+        assert (got != want.float()).float().mean().item() < 1e-3
+    else:
+        torch.testing.assert_close(got.double(), want, rtol=1e-5, atol=1e-5)
+    assert torch.all(got[:, 0:2 * Z] == 0.001) and torch.all(got[:, 100:130] == -20.0)
+    ref0 = awgn_llr(B, N, Z, sigma, seed=5, b_offset=3, qbit=qbit, device=DEV)
+    same = awgn_llr(B, N, Z, sigma, seed=5, b_offset=3, qbit=qbit, device=DEV, y=torch.zeros_like(y))
+    assert torch.equal(ref0, same)  # y = 0 is the all-zero channel, bit for bit
+
+
 @pytest.mark.parametrize("K,etha", [(3, 1.0), (7, 0.8), (70, 1.1)])
 def test_bce_multi_matches_torch(K, etha):
     """The fused device BCE (LDPCDecoderLoss's list branch) equals the reference's per-term torch
