@@ -1,6 +1,6 @@
 """Benchmark: Neural BP decoding of 5G-NR BG2 z=384 at 20 iterations (BASELINE.json configs[2]/[3]).
 
-    python bench.py [--gpus N --steps K --warmup W]            # N=1: one process
+    python bench.py [--gpus N --steps K --warmup W]            # N>1: starts N rank processes itself
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
     python bench.py --workload cfg2|cfg5                       # the other GPU configs (own lines)
 
@@ -21,6 +21,8 @@ baseline.  Rank 0 prints one JSON line.
 import argparse
 import json
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -33,6 +35,9 @@ for p in (os.path.join(ROOT, "neural-ldpc-decoder-torch_amd", "src"), ROOT):
         sys.path.insert(0, p)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, Chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles"), at the 2.4 GHz max clock
+PEAK_VALU_INSTS = 256 * 4 * 2.4e9 / 2
 METRIC = "codewords/sec + BER@Eb/N0, 5G-NR BG2 z=384, 20 iters, 1/2/4/8 MI355X"
 KINDS = ("vn", "cn", "post", "fused", "vnb", "cnb", "fusedb")
 KERNEL_NAMES = {"vn": "vn_kernel", "cn": "cn_kernel", "post": "vn_kernel (final posterior)",
@@ -62,26 +67,32 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_bytes(B, E, N, Z, T):
+def kernel_bytes(B, E, N, Z, T, train=None):
     """Algorithmic HBM bytes of one decode (all launches of a kind together), DESIGN.md §4.
 
-    fused: SURVEY.md §8(d) D5's per-codeword figure 4*(2*T*E*Z + (T+1)*N*Z) (a flooding decoder whose
-    message state is streamed once per iteration, plus the channel and the T posteriors) x B -- the
-    figure the metric's roofline is defined on; the register-resident kernel moves only the
-    compulsory part 4*(T+1)*N*Z itself (reported separately, and measured by PMC in profiles/).
-    vn/cn/post: the streaming kernels' own fp32 message traffic; vnb/cnb: the backward kernels'
-    (SURVEY D5 cfg5 model: 4*(3*E*Z + N*Z) per codeword-iteration, split VN/CN as below)."""
+    fused: the bytes the register-resident kernel must move -- the channel read once and the T
+    posteriors written, 4*(T+1)*N*Z per codeword (its message state never leaves the chip); with
+    `train` (the cfg5 SAVE variant) also what it saves for the backward per iteration: v2c (int8
+    codes for QMS: E*Z bytes), the clamp masks (N*Z bytes) and the xin chain (4*N*Z).
+    fusedb: per iteration the saved v2c, masks and xin, the output gradient, and the VN-chain carry
+    read + write (2*4*N*Z), plus the channel once.
+    vn/cn/post: the streaming kernels' fp32 message traffic; vnb/cnb: their backward."""
     f = 4
     vn_first = B * f * (E * Z + N * Z)            # read xa, write v2c (all-zero state: no c2v read)
     vn = B * f * (2 * E * Z + 2 * N * Z)          # read c2v + xa, write v2c + previous posterior
     cn = B * f * (2 * E * Z)                      # gather v2c, scatter c2v
     post = B * f * (E * Z + 2 * N * Z)            # read c2v + xa, write the last posterior
-    fused = B * f * (2 * T * E * Z + (T + 1) * N * Z)
+    fused = B * f * (T + 1) * N * Z
+    saved_it = 0
+    if train:
+        sb = 1 if train.get("qms") else 4
+        saved_it = E * Z * sb + N * Z + (4 * N * Z if train.get("vn") else 0)
+        fused += B * T * saved_it
+    fusedb = B * (f * N * Z + T * (saved_it + f * N * Z + (2 * f * N * Z if train and train.get("vn") else 0)))
     vnb = B * f * (E * Z + N * Z)                 # per iteration: grad of the posterior in, grad v2c out
     cnb = B * f * (2 * E * Z)                     # per iteration: saved v2c + grad c2v in
     return {"vn": vn_first + (T - 1) * vn, "cn": T * cn, "post": post, "fused": fused,
-            "fused_compulsory": B * f * (T + 1) * N * Z, "vnb": (T + 1) * vnb, "cnb": T * cnb,
-            "fusedb": B * f * T * (3 * E * Z + N * Z)}
+            "vnb": (T + 1) * vnb, "cnb": T * cnb, "fusedb": fusedb}
 
 
 class Prof:
@@ -107,7 +118,21 @@ class Prof:
         return {k: (ms[i], cnt[i]) for i, k in enumerate(KINDS)}
 
 
-def roofline(prof, kb, steps, B, Z, elapsed, d5_bytes_per_cw, world, graph_tag):
+def load_pmc(key):
+    """Counter totals per launch of `key` from profiles/pmc_traffic.json (written by
+    tools/pmc_summary.py from rocprofv3 --pmc passes of this bench)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        v = json.load(open(path)).get(key)
+    except (OSError, ValueError):
+        return None
+    return v if isinstance(v, dict) else None
+
+
+def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings, pmc_key):
+    """Roofline of the dominant kernel: the algorithmic bytes it must move per launch over its average
+    HIP-event launch time, against the 8 TB/s HBM spec (and the measured HBM ceilings); HBM traffic
+    and VALU issue from the committed PMC summary of the same workload when present."""
     per = {}
     for k in KINDS:
         ms_tot, n = prof[k]
@@ -115,42 +140,96 @@ def roofline(prof, kb, steps, B, Z, elapsed, d5_bytes_per_cw, world, graph_tag):
             byts = kb[k] * steps
             per[k] = {"avg_ms": ms_tot / n, "launches": n, "gbs": byts / (ms_tot / 1000.0) / 1e9,
                       "alg_bytes_per_launch": byts / n}
-            if k == "fused":
-                per[k]["compulsory_gbs"] = kb["fused_compulsory"] * steps / (ms_tot / 1000.0) / 1e9
     dom = max(per, key=lambda k: prof[k][0])
     d = per[dom]
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get(f"{dom}_B{B}_Z{Z}")
-            if isinstance(traffic, dict):
-                traffic = traffic.get("bytes")
-        except Exception:
-            traffic = None
+    pmc = load_pmc(f"{dom}_{pmc_key}")
+    traffic = pmc.get("bytes") if pmc else None
     r = {"bound": "hbm", "kernel": KERNEL_NAMES[dom].replace("<graph>", graph_tag),
          "achieved": round(d["gbs"], 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
          "frac": round(d["gbs"] / PEAK_HBM_GBS, 4), "traffic": traffic,
          "alg_bytes_per_launch": d["alg_bytes_per_launch"], "avg_launch_ms": round(d["avg_ms"], 4),
          "per_kernel": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                        for k, v in per.items()},
-         "decode_equiv_gbs_survey_formula": round(d5_bytes_per_cw * world * B * steps / elapsed / 1e9, 1)}
-    if dom == "fused":
-        # achieved uses SURVEY D5's per-codeword bytes (message state streamed once per iteration);
-        # the fused kernel keeps that state in registers/LDS, so frac can exceed 1.  The kernel's
-        # own HBM floor is the channel + T posteriors:
-        cg = d["compulsory_gbs"]
-        r["compulsory"] = {"bytes_per_launch": kb["fused_compulsory"], "achieved": round(cg, 1),
-                           "frac": round(cg / PEAK_HBM_GBS, 4)}
-        r["note"] = ("frac > 1: D5 assumes the E*Z message state streamed through HBM every iteration; "
-                     "the fused kernel keeps it on chip and is VALU-issue bound (DESIGN.md 4.1)")
+                        for k, v in per.items()}}
+    if ceilings:
+        r["measured_ceilings_gbs"] = ceilings
+        top = ceilings.get("write") if dom.startswith("fused") else ceilings.get("copy")
+        if top:
+            r["frac_of_measured_ceiling"] = round(d["gbs"] / top, 4)
+    if pmc:
+        r["pmc"] = {k: v for k, v in pmc.items() if k != "_doc"}
+        if pmc.get("valu_insts"):
+            busy = pmc["valu_insts"] / (d["avg_ms"] / 1000.0) / PEAK_VALU_INSTS
+            r["valu_issue"] = {"insts_per_launch": pmc["valu_insts"], "frac_of_peak": round(busy, 4),
+                               "peak_insts_per_s": PEAK_VALU_INSTS,
+                               "note": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x launch time)"}
+    if dom == "fused" and d5_bytes_per_cw:
+        # SURVEY §8(d) D5 models a flooding decoder whose E*Z message state crosses HBM every iteration;
+        # the fused kernel keeps that state on chip, so this is an equivalent rate, not traffic
+        eq = d5_bytes_per_cw * B / (d["avg_ms"] / 1000.0) / 1e9
+        r["d5_equivalent"] = {"bytes_per_cw": d5_bytes_per_cw, "gbs": round(eq, 1),
+                              "note": "equivalent rate of the D5 streamed-state model; not HBM traffic"}
     return r
+
+
+def hbm_ceilings(dev, gib=4.0):
+    """Measured HBM ceilings: best of 5 launches of libnldpc's 16 B/lane copy, write
+    and read probes over `gib` GiB, HIP-event timed; GB/s of bytes moved."""
+    from nldpc import _lib
+    L = _lib.lib()
+    n = int(gib * (1 << 30) // 4) // 4 * 4
+    a = torch.empty(n, dtype=torch.float32, device=dev)
+    b = torch.empty(n, dtype=torch.float32, device=dev)
+    a.fill_(1.0)
+    stream = _lib.stream_of(dev)
+    out = {}
+    for name, kind, byts in (("copy", 0, 8 * n), ("write", 1, 4 * n), ("read", 2, 4 * n), ("read_4b_lane", 3, 4 * n)):
+        best = None
+        for _ in range(6):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _lib.check(L.nldpc_hbm_probe(kind, b.data_ptr(), a.data_ptr(), n, stream), "nldpc_hbm_probe")
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        out[name] = round(byts / (best / 1000.0) / 1e9, 1)
+    del a, b
+    torch.cuda.empty_cache()
+    return out
+
+
+def launch_ranks(args):
+    """`--gpus N` with N > 1 outside a torchrun environment: start the N rank processes here (one per
+    GPU, torch.distributed.run on 127.0.0.1) before anything touches the GPU, and return their exit
+    code.  Inside a torchrun environment WORLD_SIZE must equal --gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks")
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     from nldpc import distributed as nd_dist
     rank, world, local = nd_dist.init("nccl")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but {world} rank(s) are running")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     gfile, Z, T, B = WORKLOADS[args.workload]
@@ -175,15 +254,19 @@ def timed(args, local, dev, step, prof):
     torch.cuda.synchronize(dev)
     nd_dist.barrier(local)
     torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     prof.begin()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for e0, e1 in ev:
+        e0.record()
         step()
+        e1.record()
     torch.cuda.synchronize(dev)
     nd_dist.barrier(local)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    return elapsed, prof.end()
+    step_ms = [e0.elapsed_time(e1) for e0, e1 in ev]  # per step on torch's stream (the decoder's stream)
+    return elapsed, prof.end(), step_ms
 
 
 def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
@@ -198,6 +281,7 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
     rate = (N - M) / (N - 2)  # reference code-rate formula (AWGNPassedDatagen.py:47 / neural :36)
     offset, _ = nd_dist.shard(world * B, rank, world)  # weak scaling: rank r holds [r*B, (r+1)*B)
     xa = awgn_llr(B, N, Z, sigma_for(args.ebn0, rate), seed=2042, b_offset=offset, device=dev)
+    xa_host = xa[:min(B, 2048)].cpu()  # the CPU baseline decodes these same Philox codewords
     torch.cuda.synchronize(dev)
     state = {}
 
@@ -206,8 +290,14 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
         state["outs"] = model(xa)
 
     with torch.no_grad():
-        elapsed, prof = timed(args, local, dev, step, Prof(not args.no_profile, args.steps * (2 * T + 2)))
+        elapsed, prof, step_ms = timed(args, local, dev, step, Prof(not args.no_profile, args.steps * (2 * T + 2)))
         counts = ber_counts(state["outs"])  # BER / FER per iteration, decoder convention bit = LLR > 0
+        # the reference helper itself on the same outputs (literal rule bit = LLR < 0: ~1 - BER)
+        from boosted_neural_ldpc_decoder.Functions import Functions
+        (lit_bits, _), (lit_frames, _) = Functions.evaluate_ber_fer(
+            torch.zeros((B, N * Z), dtype=torch.uint8, device=dev), state["outs"])
+        n_cpu = min(B, 2048)  # the codewords the CPU baseline may decode: their GPU outputs, kept for comparison
+        gpu_last = state["outs"][-1][:n_cpu].cpu()
         state.clear()
         # count-only decode: the same decode with the counting fused into the kernel and
         # no posteriors written -- reported beside the headline, never as `value`
@@ -218,7 +308,7 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
             def cstep():
                 cnt["c"] = model.count_errors(xa)
 
-            c_elapsed, cprof = timed(args, local, dev, cstep, Prof(not args.no_profile, args.steps + 2))
+            c_elapsed, cprof, _ = timed(args, local, dev, cstep, Prof(not args.no_profile, args.steps + 2))
             c_elapsed = nd_dist.max_time(c_elapsed, device=dev)
             count_only = {"value": round(world * B * args.steps / c_elapsed, 1), "unit": "codewords/s",
                           "ms_per_step": round(1000.0 * c_elapsed / args.steps, 3),
@@ -235,7 +325,9 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
                 sweep["bit_errors"].append(int(c[-1, 0]))
                 sweep["frame_errors"].append(int(c[-1, 1]))
                 del x
+    ceilings = hbm_ceilings(dev) if (rank == 0 and not args.no_profile) else None
     elapsed = nd_dist.max_time(elapsed, device=dev)
+    med = nd_dist.max_time(statistics.median(step_ms) / 1000.0, device=dev)
     counts = nd_dist.sum_counts(counts).cpu().numpy()  # the one RCCL exchange: BER accounting
     if rank != 0:
         return None
@@ -251,6 +343,8 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "ms_per_step_median": round(1000.0 * med, 3),
+        "value_from_median": round(world * B / med, 1),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -272,11 +366,15 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
         sweep["codewords_per_point"] = world * B
         sweep["iteration"] = T
         res["ber_sweep"] = sweep
+    # D7: Functions.evaluate_ber_fer's literal value on the same outputs (rank 0's shard; its inverted
+    # decision rule reports ~1 - BER)
+    res["ber"]["evaluate_ber_fer_literal_rank0"] = {"bit_errors_last_iter": lit_bits[-1], "bits": B * N * Z,
+                                                    "frame_errors_last_iter": lit_frames[-1], "frames": B}
     if prof is not None:
-        res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T), args.steps, B, Z, elapsed,
-                                   4 * (2 * T * E * Z + (T + 1) * N * Z), world, tag)
+        res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T), args.steps, B, Z, world, tag,
+                                   4 * (2 * T * E * Z + (T + 1) * N * Z), ceilings, f"{args.workload}_B{B}")
     if world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(bg, Z, T, sigma_for(args.ebn0, rate), args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(bg, Z, T, xa_host, gpu_last, args.cpu_seconds)
     return res
 
 
@@ -317,9 +415,10 @@ def bench_train(args, rank, world, local, dev, bg, Z, T, B):
         state["loss"] = loss.detach()
         state["last"] = outs[-1].detach()
 
-    elapsed, prof = timed(args, local, dev, step, Prof(not args.no_profile, args.steps * (6 * T + 8)))
+    elapsed, prof, step_ms = timed(args, local, dev, step, Prof(not args.no_profile, args.steps * (6 * T + 8)))
     counts = ber_counts([state["last"]])
     elapsed = nd_dist.max_time(elapsed, device=dev)
+    med = nd_dist.max_time(statistics.median(step_ms) / 1000.0, device=dev)
     counts = nd_dist.sum_counts(counts).cpu().numpy()
     if rank != 0:
         return None
@@ -331,6 +430,7 @@ def bench_train(args, rank, world, local, dev, bg, Z, T, B):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "ms_per_step_median": round(1000.0 * med, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -346,15 +446,16 @@ def bench_train(args, rank, world, local, dev, bg, Z, T, B):
                 "fer_last_iter": float(counts[-1, 1]) / (world * B)},
     }
     if prof is not None:
-        res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T), args.steps, B, Z, elapsed,
-                                   4 * (2 * T * E * Z + (T + 1) * N * Z) + 4 * T * (3 * E * Z + N * Z), world,
-                                   "bg2_z384")
+        res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T, train={"qms": True, "vn": True}), args.steps, B, Z,
+                                   world, "bg2_z384", None, None, f"{args.workload}_B{B}")
     return res
 
 
-def cpu_baseline(bg, Z, T, sigma, target_s):
+def cpu_baseline(bg, Z, T, xa_host, gpu_last, target_s):
     """Time the CPU oracle (edge-list restatement of NeuralLDPCDecoder.forward, pinned bit-exact to the
-    reference) on a bounded sample of the same workload, on this host's cores."""
+    reference; the reference itself cannot build z=384) on a bounded sample of the
+    same workload -- the first codewords of the GPU's own Philox batch -- on this host's cores, and
+    check its last-iteration output against the GPU's for those codewords."""
     from oracle.ldpc_oracle import OracleGraph, neural_forward
     try:
         avail = len(os.sched_getaffinity(0))
@@ -364,15 +465,15 @@ def cpu_baseline(bg, Z, T, sigma, target_s):
     torch.set_num_threads(cores)
     g = OracleGraph(bg, Z)
     E = g.E
+    res = {}
 
     def run(b):
-        gen = torch.Generator().manual_seed(7)
-        x = (2.0 * (-1.0 + sigma * torch.randn(b, g.N, Z, generator=gen, dtype=torch.float64)) / sigma ** 2).float()
         w = [torch.full((E,), 0.5) for _ in range(T)]
         bb = [torch.zeros(E) for _ in range(T)]
         t0 = time.perf_counter()
         with torch.no_grad():
-            neural_forward(g, x, w, bb)
+            outs = neural_forward(g, xa_host[:b], w, bb)
+        res["last"] = outs[-1]
         return time.perf_counter() - t0
 
     # scale the sample until it takes about target_s (per-call overheads make small batches slow per
@@ -381,7 +482,7 @@ def cpu_baseline(bg, Z, T, sigma, target_s):
     for _ in range(3):
         if t >= 0.6 * target_s:
             break
-        b2 = int(max(b + 1, min(2048, b * target_s / max(t, 1e-3))))
+        b2 = int(max(b + 1, min(len(xa_host), b * target_s / max(t, 1e-3))))
         if b2 <= b:
             break
         b, t = b2, run(b2)
@@ -394,9 +495,12 @@ def cpu_baseline(bg, Z, T, sigma, target_s):
                     break
     except OSError:
         pass
+    same = bool(torch.equal(res["last"], gpu_last[:b]))
     return {"value": round(b / t, 3), "unit": "codewords/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/ldpc_oracle.py neural_forward, {g.M}x{g.N} base graph z={Z}, T={T}, B={b} codewords, "
-                      f"{t:.1f} s, torch {torch.__version__} CPU, {cpu_name}"}
+            "sample": f"oracle/ldpc_oracle.py neural_forward (the reference's dense path cannot build z=384), "
+                      f"{g.M}x{g.N} base graph z={Z}, T={T}, the first B={b} codewords of the GPU's own Philox batch, "
+                      f"{t:.1f} s, torch {torch.__version__} CPU, {cpu_name}",
+            "last_iteration_equals_gpu": same}
 
 
 if __name__ == "__main__":

@@ -84,8 +84,9 @@ int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t*
 
 /* ---- execution path.  *eligible = 1 when nldpc_forward with these arguments runs the fused
  *      register-resident kernel (a base graph / lifting size compiled in, no UCN, fresh state,
- *      T <= 64, not saving for backward): then v2c is unused, and c2v is unused too with
- *      NLDPC_FLAG_NO_STATE.  Otherwise the streaming kernels run and need both buffers. */
+ *      T <= 64; saving for backward included, except QMS with an identity quantiser): then v2c is
+ *      unused, and c2v is unused too with NLDPC_FLAG_NO_STATE.  Otherwise the streaming kernels run
+ *      and need both buffers. */
 int nldpc_fast_path(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, int32_t saving,
                     int32_t* eligible);
 
@@ -197,6 +198,12 @@ int nldpc_channel_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t see
  *   3 = fused decoder, 4 = variable-node backward, 5 = check-node backward). */
 int nldpc_profile_begin(int32_t capacity);
 int nldpc_profile_end(int32_t nkinds, float* ms, int32_t* count);
+
+/* ---- benchmark instrumentation: measured HBM ceilings (SURVEY §8(d) D4 "report the measured
+ *   stream-copy ceiling too").  One launch over n floats (n % 4 == 0; 16 B per lane unless stated):
+ *   kind 0 = copy src -> dst, 1 = write-only fill of dst, 2 = read-only pass over src (dst receives
+ *   one float4 per workgroup, 8192 workgroups), 3 = read-only with 4 B per lane (dst as for 2). */
+int nldpc_hbm_probe(int32_t kind, float* dst, const float* src, int64_t n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,7 @@
 //   nldpc_ber_count  fused bit/frame error counting of a posterior (Functions.evaluate_ber_fer)
 //   nldpc_bce_loss / nldpc_bce_grad  the multi-iteration BCE training loss and its gradient
 //                    (LDPCDecoderLoss.py:70-108), one pass over all T outputs each
+//   nldpc_hbm_probe  the measured HBM ceilings the bench's roofline quotes beside the 8 TB/s spec
 #include <hip/hip_runtime.h>
 
 #include "nldpc_internal.h"
@@ -157,9 +158,56 @@ __global__ __launch_bounds__(256) void bce_grad_kernel(BceArgs a, const float* _
     }
 }
 
+// ---------------------------------------------------------------- HBM ceiling probes (bench.py roofline)
+// 16 B per lane, grid-stride, enough workgroups to cover every CU many times over.  kind 0: stream
+// copy (read + write), 1: write-only fill (the decoder's traffic is ~95 % posterior writes), 2: read
+// only (one partial sum per workgroup is written so the loads are live), 3: read only with 4 B per
+// lane, the decoder's own load width (calibrates the FETCH_SIZE counter for those loads).
+__global__ __launch_bounds__(256) void hbm_probe_kernel(int kind, float4* __restrict__ dst,
+                                                        const float4* __restrict__ src, int64_t n4) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (kind == 0) {
+        for (; i < n4; i += stride) dst[i] = src[i];
+    } else if (kind == 1) {
+        const float4 v = make_float4(1.f, 2.f, 3.f, 4.f);
+        for (; i < n4; i += stride) dst[i] = v;
+    } else {
+        float acc = 0.f;
+        if (kind == 2) {
+            for (; i < n4; i += stride) {
+                const float4 v = src[i];
+                acc += (v.x + v.y) + (v.z + v.w);
+            }
+        } else {
+            const float* s1 = reinterpret_cast<const float*>(src);
+            for (; i < 4 * n4; i += stride) acc += s1[i];
+        }
+        __shared__ float red[256];
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float s = 0.f;
+            for (int k = 0; k < 256; ++k) s += red[k];
+            dst[blockIdx.x] = make_float4(s, 0.f, 0.f, 0.f);
+        }
+    }
+}
+
 }  // namespace nldpc
 
 using namespace nldpc;
+
+extern "C" int nldpc_hbm_probe(int32_t kind, float* dst, const float* src, int64_t n, void* stream) {
+    if (kind < 0 || kind > 3 || !dst || (kind != 1 && !src) || n <= 0 || (n & 3))
+        return fail(NLDPC_EINVAL, "nldpc_hbm_probe: bad argument");
+    const int64_t n4 = n >> 2;
+    const int blocks = 256 * 32;  // 32 workgroups of 256 per CU
+    hipLaunchKernelGGL(hbm_probe_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), kind,
+                       reinterpret_cast<float4*>(dst), reinterpret_cast<const float4*>(src), n4);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NLDPC_OK : hip_fail(e, "hbm_probe_kernel launch");
+}
 
 extern "C" int nldpc_bce_workspace(int64_t n, int32_t K, size_t* bytes) {
     if (!bytes || n <= 0 || K <= 0) return fail(NLDPC_EINVAL, "nldpc_bce_workspace: bad argument");

@@ -28,7 +28,7 @@ EXPORTED = (
     "nldpc_abi_version", "nldpc_last_error", "nldpc_graph_create", "nldpc_graph_destroy", "nldpc_graph_dims",
     "nldpc_graph_edges", "nldpc_fast_path", "nldpc_saved_bytes", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
     "nldpc_awgn_llr", "nldpc_profile_begin", "nldpc_profile_end", "nldpc_bce_workspace", "nldpc_bce_loss",
-    "nldpc_bce_grad", "nldpc_forward_count", "nldpc_channel_llr",
+    "nldpc_bce_grad", "nldpc_forward_count", "nldpc_channel_llr", "nldpc_hbm_probe",
 )
 
 
@@ -85,6 +85,7 @@ def _declare(lib):
         "nldpc_awgn_llr": (_i32, [_vp, _i64, _i64, ctypes.c_float, ctypes.c_uint64, _i64, _i32, _vp]),
         "nldpc_channel_llr": (_i32, [_vp, _i64, _i64, ctypes.c_float, ctypes.c_uint64, _i64, _i32, _vp, _i64, _i64,
                                      ctypes.c_float, _i64, _i64, ctypes.c_float, _vp]),
+        "nldpc_hbm_probe": (_i32, [_i32, _vp, _vp, _i64, _vp]),
         "nldpc_profile_begin": (_i32, [_i32]),
         "nldpc_profile_end": (_i32, [_i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_i32)]),
         "nldpc_bce_workspace": (_i32, [_i64, _i32, ctypes.POINTER(ctypes.c_size_t)]),

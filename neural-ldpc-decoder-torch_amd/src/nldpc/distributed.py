@@ -40,10 +40,22 @@ def shard(total: int, rank: int, world: int):
     return offset, count
 
 
+def _all_reduce(t: torch.Tensor, op) -> torch.Tensor:
+    """all_reduce in place; device tensors go through host memory when the backend is gloo (the CPU
+    test backend, also used by the GPU test whose two ranks share one GPU)."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
+
+
 def sum_counts(counts: torch.Tensor) -> torch.Tensor:
     """All-reduce (SUM) the per-iteration (bit errors, frame errors) counters in place."""
     if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+        _all_reduce(counts, dist.ReduceOp.SUM)
     return counts
 
 
@@ -52,7 +64,7 @@ def max_time(seconds: float, device=None) -> float:
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return seconds
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    _all_reduce(t, dist.ReduceOp.MAX)
     return float(t.item())
 
 

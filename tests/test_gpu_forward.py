@@ -1,7 +1,7 @@
 """GPU parity of the forward decode (HIP kernels through the C ABI) against the reference's golden
-outputs and the CPU oracle.  Neural / MS / QMS: bit-exact soft outputs; SP: hard decisions exact,
-soft values within rtol 1e-3 / atol 5e-3 and at most 0.1 % of them beyond 1e-4 relative (device
-tanh/atanh ulps and product order, amplified by atanh near saturation).
+outputs and the CPU oracle.  Neural / MS / QMS: bit-exact soft outputs; SP: hard decisions exact and
+soft values within SURVEY §8(c) C3's SP tolerance, rtol 1e-4 / atol 2e-3, with no outlier allowance
+(sp_check).
 """
 import glob
 import os
@@ -19,13 +19,12 @@ WIMAX = np.loadtxt(os.path.join(ROOT, "resources", "wman_N0576_R34_z24.txt"), in
 DEV = torch.device("cuda")
 
 
-def sp_rel_outliers(o, ref):
-    """Fraction of SP soft values beyond the north-star 1e-4 relative agreement.  The oracle reproduces
-    the reference bit for bit (torch.prod order, tests/test_oracle_golden.py); the device differs by
-    the ulps of tanhf/atanhf (vs ATen's SLEEF / glibc) and its product order, which atanh amplifies
-    by 1/(1-P^2) near saturation: measured 0-23 of 33280 values (<= 0.07 %), DESIGN.md §6."""
-    rel = np.abs(o - ref) / np.maximum(np.abs(ref), 1e-30)
-    return float((rel > 1e-4).mean())
+def sp_check(o, ref):
+    """SP parity (north star 1e-4 relative): equal hard decisions, every soft value
+    within rtol 1e-4 / atol 2e-3 of the reference (or of the oracle, which reproduces the reference's
+    SP bit for bit: tests/test_oracle_golden.py)."""
+    assert np.array_equal(o > 0, ref > 0), f"{((o > 0) != (ref > 0)).sum()} hard decisions differ"
+    np.testing.assert_allclose(o, ref, rtol=1e-4, atol=2e-3)
 
 
 def _bg(name):
@@ -108,8 +107,7 @@ def test_boosted_forward_matches_reference(golden, name, path):
     ref = d["outputs"][:T]
     assert np.array_equal(o > 0, ref > 0)
     if kind == 0:
-        np.testing.assert_allclose(o, ref, rtol=1e-3, atol=5e-3)
-        assert sp_rel_outliers(o, ref) <= 1e-3
+        sp_check(o, ref)
     else:
         assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} soft values differ"
 

@@ -52,11 +52,8 @@ def _assert_out(o, ref, sp):
     o = o.detach().cpu().numpy()
     assert np.array_equal(o > 0, ref > 0)
     if sp:
-        np.testing.assert_allclose(o, ref, rtol=1e-3, atol=5e-3)
-        rel = np.abs(o - ref) / np.maximum(np.abs(ref), 1e-30)
-        # as test_gpu_forward.sp_rel_outliers (<= 0.1 % over a whole decode), here per single iteration's
-        # [B, N*Z] output, where a handful of saturated values is already 0.1-0.3 %
-        assert (rel > 1e-4).mean() <= 1e-2
+        from test_gpu_forward import sp_check
+        sp_check(o, ref)
     else:
         assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} soft values differ"
 
@@ -174,6 +171,14 @@ def test_awgn_llr_statistics_and_sharding():
     assert abs(noise.mean().item()) < 0.01 and abs(noise.std().item() - 1) < 0.01
     other = awgn_llr(B, N, Z, sigma, seed=12, device=DEV)
     assert not torch.equal(full, other)
+    # the device generator against its CPU restatement (oracle/philox.py, Random123-pinned Philox): the
+    # same counters and Box-Muller; fp64 log / cos / sin of the device and of glibc may differ in the
+    # last bit, which the rounding to fp32 almost always absorbs
+    from oracle.philox import awgn_llr as awgn_host
+    host = awgn_host(B // 2, N * Z, sigma, seed=11, b_offset=B // 2)
+    dev = half.reshape(B // 2, N * Z).cpu().numpy()
+    assert (dev != host).mean() < 1e-4
+    np.testing.assert_allclose(dev, host, rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.parametrize("qbit", [0, 5])
