@@ -393,7 +393,7 @@ def emit(S: Spec) -> str:
                               f"else m[{k}] = rq[{k * Z}];")
                         else:
                             w(f"            m[{k}] = rq[{k * Z}];")
-                    w(f"            cn_copy<KIND, {DC}>(m, wv, bv, a, wc);")
+                    w(f"            cn_copy<KIND, {DC}>(m, wv, bv, a, wc, {i});")
                     for k, e in enumerate(es):
                         if e in d1set:
                             j = int(S.hb_cols[e])
@@ -738,7 +738,7 @@ def emit_bwd(S: Spec) -> str:
         w("}")
 
     # ---------------------------------------------------------------- check-node backward (table driven)
-    tab, shifts, groups = [], [], {}
+    tab, rowid, shifts, groups = [], [], [], {}
     for p in range(S.P):
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
             gl = []
@@ -747,8 +747,10 @@ def emit_bwd(S: Spec) -> str:
                 sel = [i for i in rows if len(S.row_edges[i]) == dc]
                 gl.append((dc, len(tab), len(sel)))
                 tab += [S.row_edges[i][0] for i in sel]
+                rowid += sel
             groups[(p, ci)] = gl
     w(f"static __constant__ int32_t cn_tab[{max(1, len(tab))}] = {{{', '.join(str(x) for x in tab) or '0'}}};")
+    w(f"static __constant__ int32_t cn_row[{max(1, len(rowid))}] = {{{', '.join(str(x) for x in rowid) or '0'}}};")
     w(f"static __constant__ int32_t e_shift[{E}] = {{{', '.join(str(int(x)) for x in S.shift)}}};")
     w("template <int KIND, int DC>")
     w("__device__ __forceinline__ void cnb_rows(float* lds, int u, const FusedBwdArgs& a, int it, int t0, int n, "
@@ -798,7 +800,7 @@ def emit_bwd(S: Spec) -> str:
     w("                    gc[k] = rp[k * Z + q * ZT];")
     w("                }")
     w("                cn_backward<DC, KIND, false>(m, gc, DC, 0.f, wv, wv, bv, wc != nullptr, false, a.qbit, a.lo, a.hi, "
-      "gm, gw, gu, gb);")
+      "gm, gw, gu, gb, SpRow{a.sp_plan + cn_row[t0 + r] * kSpPlanBytes, a.tanh});")
     w("#pragma unroll")
     w("                for (int k = 0; k < DC; ++k) {")
     w("                    rp[k * Z + q * ZT] = gm[k];")

@@ -226,7 +226,7 @@ __device__ __forceinline__ void cnb_body(const CNBArgs& a, const Geo& q, const i
         bb[k] = (k < d && a.bias) ? a.bias[beg + k] : 0.f;
     }
     cn_backward<DC, KIND, UCN>(m, gc, d, u, wc, wu, bb, a.w_cn != nullptr, a.w_ucn != nullptr, a.qbit, a.lo, a.hi, gm,
-                               gw, gu, gb);
+                               gw, gu, gb, SpRow{a.g.sp_plan + q.node * kSpPlanBytes, a.g.tanh});
     if (q.ok) {
 #pragma unroll
         for (int k = 0; k < DC; ++k)
@@ -295,11 +295,18 @@ static hipError_t launch_cnb(const CNBArgs& a, hipStream_t s) {
     dim3 grid, block;
     node_geometry(a.B, a.g.Z, a.g.M, grid, block);
     prof_start(PROF_CNB, s);
-    switch (deg_max_bucket(a.g.max_dc)) {
-        case 12: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 12>), grid, block, 0, s, a); break;
-        case 16: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 16>), grid, block, 0, s, a); break;
-        case 24: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 24>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 32>), grid, block, 0, s, a); break;
+    // SP's check node (DC^2 ordered products per copy) is instantiated for two degree buckets only
+    const int bucket = deg_max_bucket(a.g.max_dc);
+    if constexpr (KIND == NLDPC_SP) {
+        if (bucket <= 16) hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 16>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 32>), grid, block, 0, s, a);
+    } else {
+        switch (bucket) {
+            case 12: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 12>), grid, block, 0, s, a); break;
+            case 16: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 16>), grid, block, 0, s, a); break;
+            case 24: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 24>), grid, block, 0, s, a); break;
+            default: hipLaunchKernelGGL((cnb_kernel<KIND, UCN, 32>), grid, block, 0, s, a); break;
+        }
     }
     prof_stop(s);
     return hipGetLastError();
@@ -393,6 +400,8 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
     a.w_cn = w_cn;
     a.bias = bias;
     a.w_vn = (g_w_vn && cfg->vn_cumulative) ? w_vn : nullptr;  // the chain only feeds dL/dw_vn
+    a.sp_plan = g->dev.sp_plan;
+    a.tanh = g->dev.tanh;
     a.sv2c = sb + SL.v2c_off;
     a.symask = SL.has_ymask ? reinterpret_cast<const uint8_t*>(sb + SL.ymask_off) : nullptr;
     a.sxin = SL.has_xin ? reinterpret_cast<const float*>(sb + SL.xin_off) : nullptr;

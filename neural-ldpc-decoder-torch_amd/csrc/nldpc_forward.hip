@@ -139,7 +139,7 @@ __device__ __forceinline__ void cn_body(const CNArgs& a, const Geo& q, const int
     }
     const float u = UCN ? ucn_flag<DC, KIND>(a.g, beg, d, vv, b, a.app, a.xa, a.w_vn0, a.qbit) : 0.f;
     CnCore<DC> core;
-    cn_core<DC, KIND>(m, d, a.qbit, a.lo, a.hi, core);
+    cn_core<DC, KIND>(m, d, a.qbit, a.lo, a.hi, core, SpRow{a.g.sp_plan + q.node * kSpPlanBytes, a.g.tanh});
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
         if (k < d) {
@@ -193,11 +193,18 @@ template <int KIND, bool UCN>
 static hipError_t cn_launch_k(const CNArgs& a, hipStream_t s) {
     dim3 grid, block;
     node_geometry(a.B, a.g.Z, a.g.M, grid, block);
-    switch (deg_max_bucket(a.g.max_dc)) {
-        case 12: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 12>), grid, block, 0, s, a); break;
-        case 16: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 16>), grid, block, 0, s, a); break;
-        case 24: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 24>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 32>), grid, block, 0, s, a); break;
+    // SP's check node (DC^2 ordered products per copy) is instantiated for two degree buckets only
+    const int bucket = deg_max_bucket(a.g.max_dc);
+    if constexpr (KIND == NLDPC_SP) {
+        if (bucket <= 16) hipLaunchKernelGGL((cn_kernel<KIND, UCN, 16>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((cn_kernel<KIND, UCN, 32>), grid, block, 0, s, a);
+    } else {
+        switch (bucket) {
+            case 12: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 12>), grid, block, 0, s, a); break;
+            case 16: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 16>), grid, block, 0, s, a); break;
+            case 24: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 24>), grid, block, 0, s, a); break;
+            default: hipLaunchKernelGGL((cn_kernel<KIND, UCN, 32>), grid, block, 0, s, a); break;
+        }
     }
     return hipGetLastError();
 }
@@ -231,6 +238,9 @@ int validate_cfg(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t 
     if (B > 0x7FFFFFFFLL) return fail(NLDPC_EUNSUPPORTED, "batch too large for one launch (split the batch)");
     if (cfg->vn_prefix < 0 || (cfg->vn_prefix > 0 && !cfg->vn_cumulative))
         return fail(NLDPC_EINVAL, "vn_prefix needs vn_cumulative");
+    if (cfg->kind == NLDPC_SP && !g->dev.tanh.idx)
+        return fail(NLDPC_EUNSUPPORTED, "the SP decoder needs lib/nldpc_tanh_ref.bin (built by gen_tanh_table.py with "
+                                        "the library): torch.tanh's exact values");
     return NLDPC_OK;
 }
 
@@ -275,6 +285,8 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     fa.bias = bias;
     fa.w_vn = cfg->vn_cumulative ? w_vn : nullptr;
     fa.vn_prefix = cfg->vn_prefix;
+    fa.sp_plan = g->dev.sp_plan;
+    fa.tanh = g->dev.tanh;
     fa.lo = cfg->llr_lo;
     fa.hi = cfg->llr_hi;
     fa.c2v_out = (cfg->flags & NLDPC_FLAG_NO_STATE) ? nullptr : c2v;

@@ -22,6 +22,8 @@ struct FusedArgs {
     const float* w_vn;   // [vn_prefix + T][N] or nullptr
     int32_t vn_prefix;
     float lo, hi;
+    const uint8_t* sp_plan;  // [M][kSpPlanBytes] SP product order (DevGraph::sp_plan)
+    TanhRef tanh;            // torch.tanh table (SP)
     float* c2v_out;      // [B][E][Z] final message state, or nullptr
     // what the backward needs (SAVE kernels only; SavedLayout in nldpc_internal.h)
     char* sv2c;          // [T][B][E][Z] v2c of every iteration (fp32; QMS: int8 codes, qms_code)
@@ -168,6 +170,8 @@ struct FusedBwdArgs {
     const float* w_cn;     // [T][E] or nullptr
     const float* bias;     // [T][E] (Neural) or nullptr
     const float* w_vn;     // [T][N] or nullptr
+    const uint8_t* sp_plan;  // SP product order (DevGraph::sp_plan)
+    TanhRef tanh;            // torch.tanh table (SP)
     const char* sv2c;      // saved [T][B][E][Z] (fp32; QMS: int8 codes)
     const uint8_t* symask; // saved [T][B][N][Z] or nullptr (Neural)
     const float* sxin;     // saved [T][B][N][Z] or nullptr
@@ -314,14 +318,14 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
 // specialised neural_row, MS / QMS through boosted_row, SP through the shared cn_core + cn_epilogue
 template <int KIND, int DC>
 __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], const float (&bv)[DC],
-                                        const FusedArgs& a, bool has_w) {
+                                        const FusedArgs& a, bool has_w, int row) {
     if constexpr (KIND == NLDPC_NEURAL) {
         neural_row<DC>(m, wv, bv);
     } else if (KIND == NLDPC_MS || (KIND == NLDPC_QMS && qms_active_q(a.qbit))) {
         boosted_row<DC, KIND>(m, wv, has_w, a.qbit, a.lo, a.hi);
     } else {
         CnCore<DC> core;
-        cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core);
+        cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core, SpRow{a.sp_plan + row * kSpPlanBytes, a.tanh});
 #pragma unroll
         for (int k = 0; k < DC; ++k)
             m[k] = cn_epilogue<KIND, false>(core.out0[k], wv[k], 0.f, 0.f, 0.f, has_w, false, a.qbit, a.lo, a.hi).c;

@@ -8,9 +8,15 @@
 // s = Hb[i][j] mod Z.  Row (i, h) of the lifted H has its 1 at column (j, (h + s) mod Z)
 // (lifting_matrix_1/2, ConnectingMatrix.py:84-99).  Columns list their edges in ascending check
 // row, which is the accumulation order the reference's sgemm produces.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <numeric>
 #include <string>
 #include <vector>
 
@@ -31,6 +37,94 @@ int fail(int code, const std::string& msg) {
 int hip_fail(hipError_t e, const char* what) {
     g_last_error = std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ") at " + what;
     return NLDPC_EHIP;
+}
+
+// ---- torch.tanh table (gen_tanh_table.py): loaded once per device from next to libnldpc.so (or
+// $NLDPC_TANH_TABLE), kept for the life of the process
+static std::string tanh_table_path() {
+    if (const char* p = std::getenv("NLDPC_TANH_TABLE")) return p;
+    Dl_info info;
+    if (dladdr(reinterpret_cast<void*>(&tanh_ref_table), &info) && info.dli_fname) {
+        std::string so = info.dli_fname;
+        const size_t k = so.rfind('/');
+        return (k == std::string::npos ? std::string(".") : so.substr(0, k)) + "/nldpc_tanh_ref.bin";
+    }
+    return "nldpc_tanh_ref.bin";
+}
+
+TanhRef tanh_ref_table(int device) {
+    static std::mutex mu;
+    static std::vector<std::pair<int, TanhRef>> loaded;
+    std::lock_guard<std::mutex> lock(mu);
+    for (auto& p : loaded)
+        if (p.first == device) return p.second;
+    TanhRef t{};
+    std::vector<uint32_t> buf;
+    if (FILE* f = std::fopen(tanh_table_path().c_str(), "rb")) {
+        uint32_t h[6];
+        if (std::fread(h, 4, 6, f) == 6 && h[0] == 0x4841544Eu && h[1] == 1u) {
+            const size_t nidx = (h[3] >> h[2]) + 2, n = nidx + h[4] + 2 * (size_t)h[5];
+            buf.resize(n);
+            if (std::fread(buf.data(), 4, n, f) == n) {
+                void* d = nullptr;
+                DeviceGuard guard(device);
+                if (hipMalloc(&d, n * 4) == hipSuccess && hipMemcpy(d, buf.data(), n * 4, hipMemcpyHostToDevice) == hipSuccess) {
+                    const uint32_t* b = static_cast<const uint32_t*>(d);
+                    t = TanhRef{b, b + nidx, b + nidx + h[4], (int32_t)h[5], (int32_t)h[2], h[3]};
+                }
+            }
+        }
+        std::fclose(f);
+    }
+    loaded.emplace_back(device, t);
+    return t;
+}
+
+// Product order of the SP check node.  The reference multiplies each check row's factors inside
+// torch.prod(x2_abs, dim=3) over the [B, Z, E, E] tile (BoostedNeuralLDPCDecoder.py:404): the last
+// axis runs over all E edges in V-order (column-major) with 1.0 everywhere outside the row.  ATen's
+// CPU reduction (the order oracle/ldpc_oracle.py _prod_aten restates and pins) keeps 4 accumulators
+// of 8 lanes over the first E/32*32 positions -- position p goes to accumulator (p/8)%4, lane p%8, in
+// ascending p --, combines each lane as (a0*a1)*(a2*a3), the lanes left to right, then multiplies the
+// remaining positions one by one.  Factors of exactly 1.0 change nothing, so only the row's own edges
+// matter: per row, its edges sorted by (lane, accumulator, position), tail positions last.
+static void sp_plans(int M, int E, const std::vector<int32_t>& chk, const std::vector<int32_t>& var,
+                     const std::vector<int32_t>& row_ptr, std::vector<uint8_t>& plan) {
+    std::vector<int32_t> vorder(E), vidx(E);
+    std::iota(vorder.begin(), vorder.end(), 0);
+    std::stable_sort(vorder.begin(), vorder.end(), [&](int a, int b) {
+        return var[a] != var[b] ? var[a] < var[b] : chk[a] < chk[b];
+    });
+    for (int p = 0; p < E; ++p) vidx[vorder[p]] = p;
+    const int full = E / 32 * 32;
+    plan.assign((size_t)M * kSpPlanBytes, 0);
+    for (int i = 0; i < M; ++i) {
+        const int beg = row_ptr[i], d = row_ptr[i + 1] - beg;
+        if (d > 32) continue;  // SP needs check degree <= 32 (validated at decode time)
+        std::vector<int> ord(d);
+        std::iota(ord.begin(), ord.end(), 0);
+        auto key = [&](int k) {
+            const int p = vidx[beg + k];
+            return p < full ? (int64_t)((p % 8) * 4 + (p / 8) % 4) * E + p : (int64_t)32 * E + p;
+        };
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return key(a) < key(b); });
+        uint8_t* pl = plan.data() + (size_t)i * kSpPlanBytes;
+        int prev_lane = -1;
+        for (int s = 0; s < d; ++s) {
+            const int k = ord[s], p = vidx[beg + k];
+            pl[s] = (uint8_t)k;
+            pl[32 + k] = (uint8_t)s;
+            uint8_t code;
+            if (p < full) {
+                const int lane = p % 8;
+                code = (uint8_t)(((p / 8) % 4) | (lane != prev_lane ? 4 : 0));
+                prev_lane = lane;
+            } else {
+                code = 8;
+            }
+            pl[64 + s] = code;
+        }
+    }
 }
 
 }  // namespace nldpc
@@ -79,9 +173,12 @@ extern "C" int nldpc_graph_create(int32_t M, int32_t N, int32_t Z, const int32_t
         if ((int64_t)Z * 64 > (int64_t)1 << 30)
             return fail(NLDPC_EUNSUPPORTED, "nldpc_graph_create: lifting size too large");
 
-        // one device blob: chk | var | shift | row_ptr | col_ptr | col_edge
+        std::vector<uint8_t> plan;
+        sp_plans(M, E, chk, var, row_ptr, plan);
+
+        // one device blob: chk | var | shift | row_ptr | col_ptr | col_edge | sp_plan (bytes)
         std::vector<int32_t> blob;
-        blob.reserve(3 * E + (M + 1) + (N + 1) + E);
+        blob.reserve(3 * E + (M + 1) + (N + 1) + E + plan.size() / 4);
         size_t off_chk = blob.size();
         blob.insert(blob.end(), chk.begin(), chk.end());
         size_t off_var = blob.size();
@@ -94,6 +191,9 @@ extern "C" int nldpc_graph_create(int32_t M, int32_t N, int32_t Z, const int32_t
         blob.insert(blob.end(), col_ptr.begin(), col_ptr.end());
         size_t off_cole = blob.size();
         blob.insert(blob.end(), col_edge.begin(), col_edge.end());
+        size_t off_plan = blob.size();
+        blob.resize(blob.size() + plan.size() / 4);
+        std::memcpy(blob.data() + off_plan, plan.data(), plan.size());
 
         DeviceGuard guard(device);
         void* d_blob = nullptr;
@@ -123,7 +223,8 @@ extern "C" int nldpc_graph_create(int32_t M, int32_t N, int32_t Z, const int32_t
         g->blob = d_blob;
         const int32_t* base = static_cast<const int32_t*>(d_blob);
         g->dev = DevGraph{M, N, Z, E, max_dc, max_dv, base + off_chk, base + off_var, base + off_shift,
-                          base + off_row, base + off_col, base + off_cole};
+                          base + off_row, base + off_col, base + off_cole,
+                          reinterpret_cast<const uint8_t*>(base + off_plan), tanh_ref_table(device)};
         g->h_chk = new int32_t[E];
         g->h_var = new int32_t[E];
         g->h_shift = new int32_t[E];

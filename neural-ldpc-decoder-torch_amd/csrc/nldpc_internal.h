@@ -14,6 +14,16 @@ namespace nldpc {
 //   e_chk/e_var/e_shift [E]  C-order edges (row-major over the base graph; ConnectingMatrix.py:92-99)
 //   row_ptr [M+1]            edges of check row i are the contiguous C-order range row_ptr[i]..
 //   col_ptr [N+1], col_edge  edges of column j in ascending check row (== ascending C-order index)
+//   sp_plan [M][96]          the sum-product check node's product order per row (nldpc_node.h
+//                            sp_prod_others): ord[32] | inv[32] | code[32]
+struct TanhRef {  // torch.tanh's exact fp32 results (gen_tanh_table.py); idx == nullptr: not built
+    const uint32_t* idx;
+    const uint32_t* ent;
+    const uint32_t* ovr;
+    int32_t novr, sh;
+    uint32_t kmax;
+};
+constexpr int kSpPlanBytes = 96;
 struct DevGraph {
     int32_t M, N, Z, E, max_dc, max_dv;
     const int32_t* e_chk;
@@ -22,7 +32,12 @@ struct DevGraph {
     const int32_t* row_ptr;
     const int32_t* col_ptr;
     const int32_t* col_edge;
+    const uint8_t* sp_plan;
+    TanhRef tanh;
 };
+// the process-wide device copy of lib/nldpc_tanh_ref.bin for `device` (loaded once; idx == nullptr
+// when the file is missing: SP decodes then fail with NLDPC_EUNSUPPORTED)
+TanhRef tanh_ref_table(int device);
 
 }  // namespace nldpc
 

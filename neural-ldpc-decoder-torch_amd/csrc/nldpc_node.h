@@ -10,8 +10,88 @@
 
 #include "nldpc_internal.h"
 #include "nldpc_math.h"
+#include "nldpc_sleef.h"
 
 namespace nldpc {
+
+// ---- sum-product check node arithmetic, value for value the reference's CPU tensors
+// (BoostedNeuralLDPCDecoder.py:400-408):
+//   tanh   torch.tanh of a CPU fp32 tensor: the correctly rounded value of a double tanh, corrected
+//          where torch's vector math differs by one ulp (table from gen_tanh_table.py, TanhRef)
+//   prod   torch.prod(dim=3) in ATen's reduction order (sp_prod_others, the per-row plan of
+//          nldpc_graph.cpp sp_plans)
+//   atanh  ATen's vectorised atanh, SLEEF's Sleef_atanhf16_u10 (nldpc_sleef.h)
+__device__ __noinline__ float tanh_ref(float x, TanhRef t) {
+    const uint32_t key = __float_as_uint(x) & 0x7fffffffu;
+    uint32_t r = __float_as_uint((float)tanh((double)__uint_as_float(key)));
+    if (key <= t.kmax) {
+        const uint32_t b = key >> t.sh;
+        uint32_t lo = t.idx[b], hi = t.idx[b + 1];
+        const uint32_t end = hi;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((t.ent[mid] & 0x7fffffffu) < key) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo < end && (t.ent[lo] & 0x7fffffffu) == key) r = (t.ent[lo] >> 31) ? r + 1u : r - 1u;
+        for (int i = 0; i < t.novr; ++i)
+            if (t.ovr[2 * i] == key) r = t.ovr[2 * i + 1];
+    }
+    return __uint_as_float(r | (__float_as_uint(x) & 0x80000000u));
+}
+
+__device__ __noinline__ float atanh_ref(float x) { return nldpc_sleef::atanhf_u10(x); }
+
+// Product of a row's SP factors except the sorted position sk, in ATen's order: ts holds the row's
+// factors sorted by (lane, accumulator, position) (plan ord), code[s] = accumulator (bits 0-1) | a new
+// lane starts at s (bit 2) | tail position (bit 3).  Every product the reference forms with a factor
+// of exactly 1.0 (the other rows' entries, the masked self entry) is exact, so it is skipped.
+template <int DC>
+__device__ __forceinline__ void sp_step(float v, int c, float& P, float& a0, float& a1, float& a2, float& a3, bool& open) {
+    // branch-free (selects): the code bytes are runtime values, and a branchy step unrolled DC^2 times
+    // per check copy multiplied the kernels' control flow
+    const bool tail = (c & 8) != 0;
+    const int j = c & 3;
+    const bool flush = open && (tail || (c & 4) != 0);
+    P = flush ? fmul(P, fmul(fmul(a0, a1), fmul(a2, a3))) : P;
+    a0 = flush ? 1.f : a0;
+    a1 = flush ? 1.f : a1;
+    a2 = flush ? 1.f : a2;
+    a3 = flush ? 1.f : a3;
+    const float tgt = tail ? P : (j == 0 ? a0 : (j == 1 ? a1 : (j == 2 ? a2 : a3)));
+    const float pr = fmul(tgt, v);
+    P = tail ? pr : P;
+    a0 = (!tail && j == 0) ? pr : a0;
+    a1 = (!tail && j == 1) ? pr : a1;
+    a2 = (!tail && j == 2) ? pr : a2;
+    a3 = (!tail && j == 3) ? pr : a3;
+    open = !tail;
+}
+
+// (Check degrees above 16 -- the 24 / 32 buckets of the streaming kernels -- run the loop rolled: SP
+// there is rare, and unrolling DC^2 work per check copy for them dominated the library's build.)
+template <int DC>
+__device__ __forceinline__ float sp_prod_others(const float (&ts)[DC], int d, int sk, const uint8_t* code) {
+    float P = 1.f, a0 = 1.f, a1 = 1.f, a2 = 1.f, a3 = 1.f;
+    bool open = false;
+    if constexpr (DC > 16) {
+#pragma unroll 1
+        for (int s = 0; s < d; ++s) sp_step<DC>(s == sk ? 1.f : ts[s], code[s], P, a0, a1, a2, a3, open);
+    } else {
+#pragma unroll
+        for (int s = 0; s < DC; ++s)
+            if (s < d) sp_step<DC>(s == sk ? 1.f : ts[s], code[s], P, a0, a1, a2, a3, open);
+    }
+    if (open) P = fmul(P, fmul(fmul(a0, a1), fmul(a2, a3)));
+    return P;
+}
+
+// what the SP check node of one row needs: the row's plan (kSpPlanBytes: ord | inv | code) and the
+// tanh table
+struct SpRow {
+    const uint8_t* plan;
+    TanhRef tanh;
+};
 
 // Launch geometry shared by all node kernels: blockDim = (Vt copies, Bt codewords); grid =
 // (ceil(B/Bt), nodes, ceil(Z/Vt)).  The node index (column j / check row i) is blockIdx.y, so a
@@ -122,28 +202,49 @@ struct CnCore {
     int idx1, idx2;  // first-index argmins (torch.min tie-break); -1 = none below the mask value
 };
 
+// the row's SP factors sorted by the plan (ts[s] = mq[ord[s]])
+template <int DC>
+__device__ __forceinline__ void sp_sorted(const float (&mq)[DC], int d, const uint8_t* plan, float (&ts)[DC]) {
+    if constexpr (DC > 16) {
+        for (int s = 0; s < DC; ++s) ts[s] = s < d ? mq[plan[s]] : 1.f;
+    } else {
+#pragma unroll
+        for (int s = 0; s < DC; ++s) {
+            float v = 1.f;
+            if (s < d) {
+                const int o = plan[s];
+#pragma unroll
+                for (int l = 0; l < DC; ++l) v = (l == o) ? mq[l] : v;
+            }
+            ts[s] = v;
+        }
+    }
+}
+
 template <int DC, int KIND>
-__device__ __forceinline__ void cn_core(const float (&m)[DC], int d, int qbit, float lo, float hi, CnCore<DC>& c) {
-    if (KIND == NLDPC_SP) {
+__device__ __forceinline__ void cn_core(const float (&m)[DC], int d, int qbit, float lo, float hi, CnCore<DC>& c,
+                                        const SpRow& sp) {
+    if constexpr (KIND == NLDPC_SP && DC > 32) {
+        return;  // validate_cfg rejects check degrees above 32 (the 64 bucket is never launched)
+    } else if (KIND == NLDPC_SP) {
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             if (k < d) {
                 const float x = clampf(m[k], lo, hi);
-                const float t = tanhf(fmul(-0.5f, x));
+                const float t = tanh_ref(fmul(-0.5f, x), sp.tanh);
                 c.mq[k] = fadd(t, (fabsf(t) > 0.f) ? 0.f : 1.f);
             } else {
                 c.mq[k] = 1.f;
             }
         }
+        float ts[DC];
+        sp_sorted<DC>(c.mq, d, sp.plan, ts);
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             if (k < d) {
-                float P = 1.f;
-#pragma unroll
-                for (int l = 0; l < DC; ++l)
-                    if (l < d && l != k) P = fmul(P, c.mq[l]);
+                float P = sp_prod_others<DC>(ts, d, sp.plan[32 + k], sp.plan + 64);
                 P = clampf(P, -kSpClip, kSpClip);
-                c.out0[k] = fmul(-2.f, atanhf(P));
+                c.out0[k] = fmul(-2.f, atanh_ref(P));
             } else {
                 c.out0[k] = 0.f;
             }
@@ -273,9 +374,9 @@ template <int DC, int KIND, bool UCN>
 __device__ __forceinline__ void cn_backward(const float (&m)[DC], const float (&gc)[DC], int d, float u,
                                             const float (&wc)[DC], const float (&wu)[DC], const float (&bb)[DC],
                                             bool has_w, bool has_u, int qbit, float lo, float hi, float (&gm)[DC],
-                                            float (&gw)[DC], float (&gu)[DC], float (&gb)[DC]) {
+                                            float (&gw)[DC], float (&gu)[DC], float (&gb)[DC], const SpRow& sp) {
     CnCore<DC> core;
-    cn_core<DC, KIND>(m, d, qbit, lo, hi, core);
+    cn_core<DC, KIND>(m, d, qbit, lo, hi, core, sp);
 
     const QRange qr = q_range(qbit);
     float gout[DC];  // dL/dx_output_0 per edge
@@ -318,16 +419,14 @@ __device__ __forceinline__ void cn_backward(const float (&m)[DC], const float (&
     }
 
     if (KIND == NLDPC_SP) {
-        float graw[DC];
+        float graw[DC], ts[DC];
 #pragma unroll
         for (int l = 0; l < DC; ++l) graw[l] = 0.f;
+        sp_sorted<DC>(core.mq, d, sp.plan, ts);
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             if (k < d) {
-                float P = 1.f;
-#pragma unroll
-                for (int l = 0; l < DC; ++l)
-                    if (l < d && l != k) P = fmul(P, core.mq[l]);
+                const float P = sp_prod_others<DC>(ts, d, sp.plan[32 + k], sp.plan + 64);
                 const float Pc = clampf(P, -kSpClip, kSpClip);
                 // d(-2 atanh(P))/dP = -2 / (1 - P^2); clamp passes on the closed interval
                 const float gP = gout[k] * (-2.f / (1.f - Pc * Pc)) * in_range(P, -kSpClip, kSpClip);
@@ -340,7 +439,7 @@ __device__ __forceinline__ void cn_backward(const float (&m)[DC], const float (&
         for (int l = 0; l < DC; ++l) {
             if (l < d) {
                 const float xc = clampf(m[l], lo, hi);
-                const float t = tanhf(fmul(-0.5f, xc));
+                const float t = tanh_ref(fmul(-0.5f, xc), sp.tanh);
                 gm[l] = graw[l] * (1.f - t * t) * -0.5f * in_range(m[l], lo, hi);
             } else {
                 gm[l] = 0.f;

@@ -168,3 +168,19 @@ def test_prod_order_model_matches_torch_prod(E):
     ref = torch.prod(t, dim=3)
     got = _prod_aten(t, list(range(E)), E)
     assert torch.equal(got, ref), f"{(got != ref).sum().item()} of {ref.numel()} products differ"
+
+
+def test_tanh_table_reproduces_torch_tanh():
+    """The recorded torch.tanh values (gen_tanh_table.py, used by the device SP check node and by the
+    oracle) equal this host's torch.tanh -- the function the reference's SP calls -- on random inputs
+    of the check node's domain |x| <= 10 and on the table's own correction points."""
+    from oracle import ldpc_oracle as lo
+    tab = lo._tanh_table()
+    if tab is None:
+        pytest.skip("lib/nldpc_tanh_ref.bin not built")
+    gen = torch.Generator().manual_seed(11)
+    x = torch.cat([(torch.rand(1 << 20, generator=gen) * 20 - 10),
+                   torch.from_numpy(tab[0][::97].astype(np.int32)).view(torch.float32)])
+    x = torch.cat([x, -x])
+    got = lo._tanh(x)
+    assert torch.equal(got, torch.tanh(x)), f"{(got != torch.tanh(x)).sum().item()} values differ"
