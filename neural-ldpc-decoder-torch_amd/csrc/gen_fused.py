@@ -36,6 +36,9 @@ CN_PAIR_MAXDC = int(os.environ.get("NLDPC_GEN_CNPAIR", "0"))
 # build): a v_pk_add_f32 occupies the SIMD for 8 cycles against 2 for v_add_f32, so packing costs
 # time per element; scalar is the default
 PACK_VN = os.environ.get("NLDPC_GEN_PACK") == "1"
+# experiment knob: no opaque row base in the check-node phase (lets the compiler prove the row copies'
+# LDS slots disjoint and overlap them, at its own register cost)
+NORO = os.environ.get("NLDPC_GEN_NORO") == "1"
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q)
 SPECS = [
@@ -385,7 +388,8 @@ def emit(S: Spec) -> str:
                     w("        {  // one check copy at a time: the state owns the registers")
                     w(f"            float m[{DC}];")
                     w(f"            int ro = {(e0 - e0c) * Z + q * ZT} + u;  // one base VGPR per row copy: the edges ride in")
-                    w("            asm volatile(\"\" : \"+v\"(ro));  // the 16-bit DS offset")
+                    if not NORO:
+                        w("            asm volatile(\"\" : \"+v\"(ro));  // the 16-bit DS offset")
                     w("            float* rq = lds + ro;")
                     for k, e in enumerate(es):
                         if e in d1set:
