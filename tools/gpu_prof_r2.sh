@@ -1,0 +1,22 @@
+# GPU-box script: rocprofv3 kernel-trace summaries and PMC passes (one counter group per run, with
+# --kernel-trace only, as MI355X_MICROARCH.md prescribes) for cfg3 and cfg5, plus the probe kernels
+# that calibrate FETCH_SIZE / WRITE_SIZE.  Library built on the CPU side.
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
+TAG=${TAG:-r2}
+cd /tmp && export TMPDIR=/tmp
+run() {  # name, timeout, rocprof args..., -- command
+    local name=$1 t=$2; shift 2
+    timeout -k 10 $t rocprofv3 "$@" > $O/${TAG}_${name}.log 2>&1 || { echo "$name failed rc=$?"; tail -5 $O/${TAG}_${name}.log; exit 1; }
+    echo "$name ok"
+}
+B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-sweep --no-count-only"
+run probe_fetch 120 --pmc FETCH_SIZE --kernel-trace -d $O/${TAG}_probe_fetch -o run --output-format csv -- python3 $R/tools/probe_pmc.py
+run probe_write 120 --pmc WRITE_SIZE --kernel-trace -d $O/${TAG}_probe_write -o run --output-format csv -- python3 $R/tools/probe_pmc.py
+for W in cfg3 cfg5; do
+    run ${W}_trace 300 --kernel-trace --stats -d $O/${TAG}_${W}_trace -o run --output-format csv -- $B --workload $W
+    run ${W}_fetch 300 --pmc FETCH_SIZE --kernel-trace -d $O/${TAG}_${W}_fetch -o run --output-format csv -- $B --workload $W --no-profile
+    run ${W}_write 300 --pmc WRITE_SIZE --kernel-trace -d $O/${TAG}_${W}_write -o run --output-format csv -- $B --workload $W --no-profile
+    run ${W}_sq 300 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/${TAG}_${W}_sq -o run --output-format csv -- $B --workload $W --no-profile
+done
+echo "all passes done"
