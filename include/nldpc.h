@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NLDPC_ABI_VERSION 1
+#define NLDPC_ABI_VERSION 2
 
 enum nldpc_status {
     NLDPC_OK = 0,
@@ -123,6 +123,10 @@ int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t
  *   outs       forward outputs (needed for UCN flags and the output clamp mask)
  *   grad_outs  host array of T device pointers [B][N*Z] (NULL entry = zero gradient)
  *   saved      as written by nldpc_forward
+ *   grad_c2v_out [B][E][Z] gradient arriving at the final message state (the state a later segment
+ *              of the same forward resumed from: list-valued xa, split iteration runs), or NULL
+ *   grad_c2v_in  [B][E][Z] out: gradient of the incoming message state (cfg->c2v_in), or NULL
+ *              (either of the two selects the streaming backward)
  *   g_w_cn, g_w_ucn, g_bias: [T][E] accumulated (+=) per-edge gradients, NULL if not wanted
  *   g_w_vn     [vn_prefix + T][N] accumulated (+=) per-column gradients, NULL if not wanted
  *   work       device scratch of nldpc_backward_workspace() bytes */
@@ -131,8 +135,8 @@ int nldpc_backward_workspace(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
 int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
                    const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
                    const float* const* outs, const float* const* grad_outs, const float* app_prev,
-                   const void* saved, float* g_w_cn, float* g_w_ucn, float* g_bias, float* g_w_vn,
-                   void* work, size_t work_bytes, void* stream);
+                   const void* saved, const float* grad_c2v_out, float* grad_c2v_in, float* g_w_cn,
+                   float* g_w_ucn, float* g_bias, float* g_w_vn, void* work, size_t work_bytes, void* stream);
 
 /* ---- BER/FER accounting: replaces Functions.evaluate_ber_fer (Functions.py:85-102) and the
  *      per-iteration .item() loop of train/train_BoostedNeuralLDPCDecoder.py:363-383.

@@ -40,12 +40,67 @@ PACK_VN = os.environ.get("NLDPC_GEN_PACK") == "1"
 # LDS slots disjoint and overlap them, at its own register cost)
 NORO = os.environ.get("NLDPC_GEN_NORO") == "1"
 
-# (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q)
+# (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
+# chosen by auto_geometry
 SPECS = [
     ("bg2_z384", "basegraph2_set0.txt", 384, 1, 8, 3),
     ("bg2_z16", "basegraph2_set0.txt", 16, 16, 2, 1),
     ("wimax_z24", "wman_N0576_R34_z24.txt", 24, 16, 1, 1),
+    ("bg2_z96", "basegraph2_set0.txt", 96, None, None, None),
 ]
+# More (graph, Z) pairs at build time: NLDPC_FUSED_EXTRA="bg2:192,wimax:48,<file.txt>:Z" (base graph
+# files from resources/; bg2 / wimax name the two shipped ones).  Every other lifted graph decodes on
+# the streaming kernels.
+_GRAPH_FILES = {"bg2": "basegraph2_set0.txt", "wimax": "wman_N0576_R34_z24.txt"}
+for _item in filter(None, os.environ.get("NLDPC_FUSED_EXTRA", "").split(",")):
+    _g, _z = _item.rsplit(":", 1)
+    _f = _GRAPH_FILES.get(_g, _g)
+    _tag = f"{_g if _g in _GRAPH_FILES else os.path.splitext(os.path.basename(_g))[0]}_z{int(_z)}"
+    if all(t[0] != _tag for t in SPECS):
+        SPECS.append((_tag, _f, int(_z), None, None, None))
+
+MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
+
+
+def auto_geometry(hb, Z):
+    """(G, P, Q) for a lifted graph: G codewords x P parts x Z/Q lanes per workgroup, whole waves, at
+    most 1024 threads, at most MAX_STATE_REGS state floats per thread, check rows that fit LDS.
+    Prefers >= 512 threads, then fewer LDS chunks (fewer barriers), then more threads, then fewer
+    copies per thread."""
+    rows, cols = np.nonzero(hb != -1)
+    deg = np.bincount(cols, minlength=hb.shape[1])
+    multi = [int(d) for d in deg if d > 1]
+    row_deg = np.bincount(rows, minlength=hb.shape[0])
+    best = None
+    for Q in [q for q in range(1, Z + 1) if Z % q == 0]:
+        ZT = Z // Q
+        for G in (1, 2, 4, 8, 16, 32):
+            lanes = G * ZT
+            if lanes % 64:
+                continue
+            for P in (8, 7, 6, 5, 4, 3, 2, 1):
+                threads = P * lanes
+                if threads > 1024:
+                    continue
+                load = [0] * P
+                for d in sorted(multi, reverse=True):
+                    load[int(np.argmin(load))] += d
+                if Q * max(load) > MAX_STATE_REGS:
+                    continue
+                cap = (LDS_BYTES // (4 * G) - 32) // Z  # edges per LDS chunk
+                if cap < int(row_deg.max()):
+                    continue
+                nchunks, acc = 1, 0
+                for d in row_deg:
+                    if acc + d > cap:
+                        nchunks, acc = nchunks + 1, 0
+                    acc += int(d)
+                key = (threads >= 512, -nchunks, threads, -Q)
+                if best is None or key > best[0]:
+                    best = (key, (G, P, Q))
+    if best is None:
+        raise SystemExit(f"gen_fused: no register-resident geometry for Z={Z}")
+    return best[1]
 
 
 def balance(items, weight, P):
@@ -924,6 +979,8 @@ def main():
     only = set(filter(None, os.environ.get("NLDPC_GEN_ONLY", "").split(",")))  # debug: subset of specs
     for tag, fname, Z, G, P, Q in SPECS:
         hb = np.loadtxt(os.path.join(res, fname), int, delimiter="\t")
+        if G is None:
+            G, P, Q = auto_geometry(hb, Z)
         specs.append((Spec(tag, hb, Z, G, P, Q), not only or tag in only))
     head = ["// GENERATED by gen_fused.py from the base graphs in resources/ -- do not edit.",
             "#include <hip/hip_runtime.h>", '#include "nldpc_fused.h"', "namespace nldpc {"]

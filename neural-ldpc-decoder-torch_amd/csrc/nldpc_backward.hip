@@ -110,6 +110,17 @@ __device__ __forceinline__ void block_edge_partials(float (&v)[NA][DC], int d, f
     }
 }
 
+// y += x (n floats)
+__global__ void add_kernel(float* __restrict__ y, const float* __restrict__ x, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] += x[i];
+}
+static hipError_t add_launch(float* y, const float* x, int64_t n, hipStream_t s) {
+    const int64_t b = (n + 255) / 256;
+    hipLaunchKernelGGL(add_kernel, dim3((unsigned)(b < 16384 ? b : 16384)), dim3(256), 0, s, y, x, n);
+    return hipGetLastError();
+}
+
 // out[r][c] += sum over b of part[r][b][c]  (r < rows, c < width), in ascending b
 __global__ void reduce_partials(const float* __restrict__ part, int64_t rows, int64_t nb, int64_t width,
                                 float* __restrict__ out) {
@@ -352,9 +363,9 @@ static hipError_t reduce_launch(const float* part, int64_t rows, int64_t nb, int
 }
 
 // ---- fused backward (register-resident kernels generated by gen_fused.py emit_bwd) ---------------
-static bool fused_bwd_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T) {
+static bool fused_bwd_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T, bool state_grads) {
     static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
-    if (disabled || (cfg->flags & NLDPC_FLAG_STREAM) || g->fused < 0) return false;
+    if (disabled || state_grads || (cfg->flags & NLDPC_FLAG_STREAM) || g->fused < 0) return false;
     if (cfg->kind == NLDPC_QMS && !qms_active(cfg->qbit)) return false;  // QMS saved state = int8 codes
     return !cfg->ucn && cfg->vn_prefix == 0 && T <= kFusedMaxT;
 }
@@ -437,19 +448,23 @@ extern "C" int nldpc_backward_workspace(const nldpc_graph* g, const nldpc_cfg* c
     int st = validate_cfg(g, cfg, B, T);
     if (st) return st;
     if (!bytes) return fail(NLDPC_EINVAL, "nldpc_backward_workspace: null output");
-    *bytes = fused_bwd_eligible(g, cfg, T) ? fused_work_layout(g, cfg, B, T).total : work_layout(g, cfg, B, T).total;
+    // enough for either path (a call with message-state gradients always streams)
+    const size_t streaming = work_layout(g, cfg, B, T).total;
+    const size_t fused = fused_bwd_eligible(g, cfg, T, false) ? fused_work_layout(g, cfg, B, T).total : 0;
+    *bytes = fused > streaming ? fused : streaming;
     return NLDPC_OK;
 }
 
 extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
                               const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
                               const float* const* outs, const float* const* grad_outs, const float* app_prev,
-                              const void* saved, float* g_w_cn, float* g_w_ucn, float* g_bias, float* g_w_vn,
-                              void* work, size_t work_bytes, void* stream) {
+                              const void* saved, const float* grad_c2v_out, float* grad_c2v_in, float* g_w_cn,
+                              float* g_w_ucn, float* g_bias, float* g_w_vn, void* work, size_t work_bytes,
+                              void* stream) {
     int st = validate_cfg(g, cfg, B, T);
     if (st) return st;
     if (!xa || !outs || !grad_outs || !saved || !work) return fail(NLDPC_EINVAL, "nldpc_backward: null argument");
-    const bool fusedb = fused_bwd_eligible(g, cfg, T);
+    const bool fusedb = fused_bwd_eligible(g, cfg, T, grad_c2v_out || grad_c2v_in);
     const WorkLayout WL = work_layout(g, cfg, B, T);
     if (work_bytes < (fusedb ? fused_work_layout(g, cfg, B, T).total : WL.total))
         return fail(NLDPC_EINVAL, "nldpc_backward: workspace too small");
@@ -487,6 +502,10 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
                    cfg->qbit};
         hipError_t e = vnb_launch(cfg->kind, va, s);
         if (e != hipSuccess) return hip_fail(e, "vnb_kernel launch");
+        if (grad_c2v_out) {  // + the gradient arriving at the final message state (a later segment's input)
+            e = add_launch(gc, grad_c2v_out, B * G.E * G.Z, s);
+            if (e != hipSuccess) return hip_fail(e, "add_kernel launch");
+        }
     }
     for (int k = T - 1; k >= 0; --k) {
         const float* app = nullptr;
@@ -511,13 +530,13 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
                    cfg->llr_hi};
         hipError_t e = cnb_launch(cfg->kind, cfg->ucn != 0, ca, s);
         if (e != hipSuccess) return hip_fail(e, "cnb_kernel launch");
-        if (k == 0 && !vn_grad) break;
+        if (k == 0 && !vn_grad && !grad_c2v_in) break;
         VNBArgs va{G,
                    B,
                    gv,
                    k >= 1 ? grad_outs[k - 1] : nullptr,
                    (k >= 1 && smask) ? smask + (int64_t)(k - 1) * SL.ymask_stride : nullptr,
-                   k >= 1 ? gc : nullptr,
+                   k >= 1 ? gc : grad_c2v_in,  // k = 0: dL/d(the incoming message state)
                    xa,
                    w_vn,
                    vn_grad ? p_vn + (int64_t)(P0 + k) * nbN : nullptr,

@@ -11,10 +11,15 @@ get their gradients from nldpc_backward.
 What is different from the reference and why:
   * no dense routing buffers are registered (W_*, Lift_Matrix*: 22.9 GB each at z=384); their keys
     in an old state_dict are ignored on load;
-  * `self.llr[t]` holds the message state in the kernel layout [B, E, Z] (reference [B, Z, E]) and
-    only at the end of each processed run of iterations (None = the initial all-zero state);
-  * a gradient through an iteration run that starts from a stored state (a segment that does not
-    begin at iteration 0) or through list-valued `xa` raises NotImplementedError.
+  * `self.llr[t]` holds the message state in the kernel layout [B, E, Z] (reference [B, Z, E]); None
+    is the initial all-zero state.  The fused kernel keeps the state on chip, so inside a run of
+    consecutive iterations the boundaries are recorded (input, weights, starting state) and the state
+    is recomputed on demand -- the value the reference stored -- when a later call resumes there
+    (e.g. forward() followed by forward(target_iter=k)).  Such a recomputed state is a constant: a
+    gradient does not flow back into the call that produced it (in the reference it would reach that
+    call's graph, which a completed backward has already freed).
+  * gradients flow through the message state between the segments of one call (list-valued xa: one
+    segment per iteration; split iteration lists), as through the reference's self.llr[t + 1].
 """
 from typing import Optional
 
@@ -91,6 +96,29 @@ class BoostedNeuralLDPCDecoder(nn.Module):
                         for _ in range(self.iter_node_counts)]
         self.llr = [None] * (self.iter_node_counts + 1)
         self._register_params()
+
+    # ------------------------------------------------------------------ message state across calls
+    class _Pending:
+        """The state after `off` iterations of a recorded run (materialised on demand)."""
+
+        def __init__(self, rec, off):
+            self.rec, self.off = rec, off
+
+    def _state(self, k):
+        """self.llr[k] as a tensor (None = all-zero), recomputing a recorded boundary state."""
+        st = self.llr[k]
+        if isinstance(st, BoostedNeuralLDPCDecoder._Pending):
+            rec, off = st.rec, st.off
+            with torch.no_grad():
+                state_in = rec["state_in"]
+                w = lambda a: None if a is None else a[:off]  # noqa: E731
+                cfg = rec["cfg"]
+                _, st = decode_autograd(self.conn_mat.graph, cfg, rec["x"], off, w_cn=w(rec["w_cn"]),
+                                        w_ucn=w(rec["w_ucn"]),
+                                        w_vn=None if rec["w_vn"] is None else rec["w_vn"][:cfg.vn_prefix + off],
+                                        c2v=state_in, app_prev=rec["app_prev"])
+            self.llr[k] = st
+        return st
 
     # ------------------------------------------------------------------ parameter registry
     def _param_name(self, param_type: ParamType, node_type: NodeType, iterative_node_identifier: int):
@@ -297,6 +325,7 @@ class BoostedNeuralLDPCDecoder(nn.Module):
             else:
                 runs.append([it])
         vn_hist = []  # VN weights already applied to xa_input in this call (cumulative, :329)
+        live = {}  # boundary -> state produced by this call (in the autograd graph, as self.llr[t + 1] is)
         for run in runs:
             x_in = xa[run[0]] if listed else xa
             if x_in.dim() != 3 or x_in.shape[0] != self.batch_size:
@@ -313,16 +342,22 @@ class BoostedNeuralLDPCDecoder(nn.Module):
             w_vn_all = torch.stack(prefix + w_vn) if has_vn else None
             app_prev = None
             if cfg.ucn and run[0] > 0:
-                app_prev = self.outputs[run[0] - 1].reshape(self.batch_size, self.N * self.Z)
-            state_in = self.llr[run[0]]
-            if (state_in is not None or listed) and torch.is_grad_enabled() and any(
-                    p.requires_grad for p in self.parameters()):
-                raise NotImplementedError("gradients through a decode resumed from a stored state or a list input")
-            outs, state = decode_autograd(self.conn_mat.graph, cfg, x_in, len(run), w_cn=stack(w_cn),
-                                          w_ucn=stack(w_ucn), w_vn=w_vn_all, c2v=state_in, app_prev=app_prev)
+                app_prev = self.outputs[run[0] - 1].reshape(self.batch_size, self.N * self.Z).detach()
+            # the state this run starts from: this call's own (differentiable) or a stored one (:343, :377)
+            state_in = live[run[0]] if run[0] in live else self._state(run[0])
+            wc, wu = stack(w_cn), stack(w_ucn)
+            outs, state = decode_autograd(self.conn_mat.graph, cfg, x_in, len(run), w_cn=wc, w_ucn=wu, w_vn=w_vn_all,
+                                          c2v=state_in, app_prev=app_prev)
             for t, o in zip(run, outs):
                 self.outputs[t] = o
-            self.llr[run[-1] + 1] = state.detach()
+            live[run[-1] + 1] = state
+            self.llr[run[-1] + 1] = state
+            if len(run) > 1:  # the boundaries inside the run: recomputed on demand (see the module docstring)
+                det = lambda a: None if a is None else a.detach()  # noqa: E731
+                rec = {"cfg": cfg, "x": x_in.detach(), "w_cn": det(wc), "w_ucn": det(wu), "w_vn": det(w_vn_all),
+                       "state_in": None if state_in is None else state_in.detach(), "app_prev": app_prev}
+                for off in range(1, len(run)):
+                    self.llr[run[0] + off] = BoostedNeuralLDPCDecoder._Pending(rec, off)
             if has_vn and not listed:
                 vn_hist = vn_hist + w_vn
 

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("NLDPC_LIB_PATH") or os.path.normpath(os.path.join(_HE
 
 NLDPC_OK, NLDPC_EINVAL, NLDPC_EHIP, NLDPC_EUNSUPPORTED = 0, 1, 2, 3
 NLDPC_SP, NLDPC_MS, NLDPC_QMS, NLDPC_NEURAL = 0, 1, 2, 3
-ABI_VERSION = 1
+ABI_VERSION = 2
 FLAG_STREAM, FLAG_FUSED, FLAG_NO_STATE = 1, 2, 4
 
 # every symbol include/nldpc.h declares
@@ -78,7 +78,7 @@ def _declare(lib):
                                  _vp, _vp, _vp]),
         "nldpc_backward_workspace": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, ctypes.POINTER(ctypes.c_size_t)]),
         "nldpc_backward": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _vp, _vp, _vp, _vp, _vp, _PP, _PP, _vp,
-                                  _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
         "nldpc_ber_count": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp]),
         "nldpc_forward_count": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                        _vp, _vp]),

@@ -130,8 +130,11 @@ def decode_count(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *
 
 
 def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, saved, *, w_cn=None, w_ucn=None,
-                    bias=None, w_vn=None, app_prev=None, need=(True, True, True, True)):
-    """Gradients of the per-edge / per-column weights.  Returns (g_w_cn, g_w_ucn, g_bias, g_w_vn)."""
+                    bias=None, w_vn=None, app_prev=None, need=(True, True, True, True), c2v_in=False,
+                    grad_state=None, want_state_grad=False):
+    """Gradients of the per-edge / per-column weights and, with want_state_grad, of the incoming message
+    state (c2v_in: the forward resumed from a state).  grad_state: gradient arriving at the final state
+    [B, E, Z] (None = zero).  Returns (g_w_cn, g_w_ucn, g_bias, g_w_vn, g_c2v_in)."""
     dev = xa.device
     B = int(xa.shape[0])
     def z(ref, on):
@@ -141,7 +144,9 @@ def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, 
     g_ucn = z(w_ucn, need[1])
     g_b = z(bias, need[2])
     g_vn = z(w_vn, need[3])
-    c = cfg.c_struct(False)
+    g_state = torch.zeros((B, graph.E, graph.Z), dtype=torch.float32, device=dev) if want_state_grad else None
+    gs_in = None if grad_state is None else grad_state.to(torch.float32).contiguous()
+    c = cfg.c_struct(c2v_in)
     L = _lib.lib()
     h = graph.handle(dev)
     nbytes = ctypes.c_size_t(0)
@@ -154,23 +159,27 @@ def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, 
     xa_c = _f32c(xa)
     w_cn, w_ucn, bias, w_vn = _f32c(w_cn), _f32c(w_ucn), _f32c(bias), _f32c(w_vn)
     st = L.nldpc_backward(h, ctypes.byref(c), B, T, _lib.ptr(xa_c), _lib.ptr(w_cn), _lib.ptr(w_ucn), _lib.ptr(bias),
-                          _lib.ptr(w_vn), po, pg, _lib.ptr(_f32c(app_prev)), _lib.ptr(saved), _lib.ptr(g_cn),
-                          _lib.ptr(g_ucn), _lib.ptr(g_b), _lib.ptr(g_vn), _lib.ptr(work), int(work.numel()),
-                          _lib.stream_of(dev))
+                          _lib.ptr(w_vn), po, pg, _lib.ptr(_f32c(app_prev)), _lib.ptr(saved), _lib.ptr(gs_in),
+                          _lib.ptr(g_state), _lib.ptr(g_cn), _lib.ptr(g_ucn), _lib.ptr(g_b), _lib.ptr(g_vn),
+                          _lib.ptr(work), int(work.numel()), _lib.stream_of(dev))
     del keep1, keep2
     _lib.check(st, "nldpc_backward")
-    return g_cn, g_ucn, g_b, g_vn
+    return g_cn, g_ucn, g_b, g_vn, g_state
 
 
 class DecodeFn(torch.autograd.Function):
-    """outputs = decoder(xa; w_cn, w_ucn, bias, w_vn) with gradients for the four weight tensors.
+    """outputs, state = decoder(xa, c2v_in; w_cn, w_ucn, bias, w_vn) with gradients for the four weight
+    tensors and for the incoming message state, and the final state differentiable too -- so that
+    segments of one forward chained through the state (list-valued xa, split iteration runs;
+    BoostedNeuralLDPCDecoder.py:320-512 keeps self.llr[t+1] in the autograd graph) backpropagate
+    across segment boundaries.
 
     forward returns the T outputs as separate tensors (views of one [T, B, N*Z] buffer) plus the
-    final message state (non-differentiable)."""
+    final message state [B, E, Z] (an empty tensor when the fused path did not keep it)."""
 
     @staticmethod
-    def forward(ctx, graph, cfg, T, c2v_in, app_prev, xa, w_cn, w_ucn, bias, w_vn):
-        need_grad = any(t is not None and t.requires_grad for t in (w_cn, w_ucn, bias, w_vn))
+    def forward(ctx, graph, cfg, T, app_prev, xa, c2v_in, w_cn, w_ucn, bias, w_vn):
+        need_grad = any(t is not None and t.requires_grad for t in (c2v_in, w_cn, w_ucn, bias, w_vn))
         outs, state, saved = decode(graph, cfg, xa, T, w_cn=w_cn, w_ucn=w_ucn, bias=bias, w_vn=w_vn, c2v=c2v_in,
                                     app_prev=app_prev, save=need_grad)
         ctx.graph, ctx.cfg, ctx.T = graph, cfg, T
@@ -180,24 +189,28 @@ class DecodeFn(torch.autograd.Function):
             ctx.save_for_backward(xa, w_cn, w_ucn, bias, w_vn, app_prev, outs, saved)
         if state is None:
             state = outs.new_empty((0,))
-        ctx.mark_non_differentiable(state)
+            ctx.mark_non_differentiable(state)
         return (*outs.unbind(0), state)
 
     @staticmethod
     def backward(ctx, *grads):
         xa, w_cn, w_ucn, bias, w_vn, app_prev, outs, saved = ctx.saved_tensors
-        if ctx.has_state_in:
-            raise NotImplementedError("backward through a decode that resumed from a stored message state")
         grad_outs = list(grads[:ctx.T])
+        g_state_out = grads[ctx.T]
+        if g_state_out is not None and g_state_out.numel() == 0:
+            g_state_out = None
+        want_state = ctx.has_state_in and ctx.needs_input_grad[5]
         need = (ctx.needs_input_grad[6], ctx.needs_input_grad[7], ctx.needs_input_grad[8], ctx.needs_input_grad[9])
-        g_cn, g_ucn, g_b, g_vn = decode_backward(ctx.graph, ctx.cfg, xa, ctx.T, grad_outs, outs.unbind(0), saved,
-                                                 w_cn=w_cn, w_ucn=w_ucn, bias=bias, w_vn=w_vn, app_prev=app_prev,
-                                                 need=need)
-        return (None, None, None, None, None, None, g_cn if need[0] else None, g_ucn if need[1] else None,
-                g_b if need[2] else None, g_vn if need[3] else None)
+        g_cn, g_ucn, g_b, g_vn, g_c2v = decode_backward(
+            ctx.graph, ctx.cfg, xa, ctx.T, grad_outs, outs.unbind(0), saved, w_cn=w_cn, w_ucn=w_ucn, bias=bias,
+            w_vn=w_vn, app_prev=app_prev, need=need, c2v_in=ctx.has_state_in, grad_state=g_state_out,
+            want_state_grad=want_state)
+        return (None, None, None, None, None, g_c2v if want_state else None, g_cn if need[0] else None,
+                g_ucn if need[1] else None, g_b if need[2] else None, g_vn if need[3] else None)
 
 
 def decode_autograd(graph, cfg, xa, T, *, w_cn=None, w_ucn=None, bias=None, w_vn=None, c2v=None, app_prev=None):
-    """Differentiable decode.  Returns (list of T outputs [B, N*Z], final state [B, E, Z])."""
-    res = DecodeFn.apply(graph, cfg, T, c2v, app_prev, xa, w_cn, w_ucn, bias, w_vn)
+    """Differentiable decode.  Returns (list of T outputs [B, N*Z], final state [B, E, Z]).  c2v: the
+    incoming message state (None = all-zero); gradients flow into it when it requires grad."""
+    res = DecodeFn.apply(graph, cfg, T, app_prev, xa, c2v, w_cn, w_ucn, bias, w_vn)
     return list(res[:T]), res[T]

@@ -1,0 +1,69 @@
+"""The stateful forward contracts of BoostedNeuralLDPCDecoder on the GPU against the
+reference's own results (tests/golden/gen_golden_f3.py): list-valued xa, a call that resumes from the
+state another call stored (self.llr, BoostedNeuralLDPCDecoder.py:343, 377, 512) -- also from the
+middle of that call's iterations --, and a split iteration list.  The last call of each sequence runs
+with gradients: outputs bit-exact, LDPCDecoderLoss BCE value rtol 1e-6, parameter gradients rtol 1e-4
+(batch-sum order)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+BG2 = np.loadtxt(os.path.join(ROOT, "resources", "basegraph2_set0.txt"), int, delimiter="\t")
+DEV = torch.device("cuda")
+CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "stateful_*.npz")))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_stateful_sequence_matches_reference(golden, name):
+    import boosted_neural_ldpc_decoder as bd
+    from boosted_neural_ldpc_decoder.BoostedNeuralLDPCDecoder import BoostedNeuralLDPCDecoder
+    from boosted_neural_ldpc_decoder.LDPCDecoderLoss import LDPCDecoderLoss
+    from boosted_neural_ldpc_decoder.struct.DecoderType import DecoderType
+    from boosted_neural_ldpc_decoder.struct.LossType import LossType
+    from boosted_neural_ldpc_decoder.struct.NodeWeightSharingConfig import NodeWeightSharingConfig as NW
+    d = golden(name)
+    T, Z = int(d["T"]), int(d["Z"])
+    B = d["x0"].shape[0]
+    conn = bd.ConnectingMatrixTorch(bd.ConnectingMatrix(Z, BG2), device=DEV)
+    model = BoostedNeuralLDPCDecoder(T, B, conn, node_weight_sharing_config=NW(*[int(v) for v in d["nw"]]),
+                                     decoding_type=DecoderType(int(d["dtype"])), decoder_qms_qbit=int(d["q"])).to(DEV)
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            p.copy_(torch.from_numpy(d["param__" + n]))
+    ncalls = int(d["ncalls"])
+    for c in range(ncalls):
+        iters = [int(v) for v in d[f"call{c}_iters"]]
+        sel = [int(v) for v in d[f"call{c}_x"]]
+        listed = bool(int(d[f"call{c}_listed"]))
+        xin = [torch.from_numpy(d[f"x{k}"]).to(DEV) for k in sel] if listed else torch.from_numpy(d[f"x{sel[0]}"]).to(DEV)
+        kw = {"fixed_iter": []} if listed else {}
+        if c < ncalls - 1:
+            with torch.no_grad():
+                model(xin, target_iter=list(iters), **kw)
+            continue
+        outs = model(xin, target_iter=list(iters), **kw)
+        y = torch.from_numpy(d["y"].astype(np.float32)).to(DEV)
+        loss = LDPCDecoderLoss(loss_type=LossType.BCE, etha=1.0)(outs, y, coeff_param=list(range(len(outs))))
+        loss.backward()
+    got = np.stack([o.detach().cpu().numpy() for o in outs])
+    assert np.array_equal(got, d["outputs"]), f"{(got != d['outputs']).sum()} of {got.size} soft values differ"
+    np.testing.assert_allclose(loss.item(), float(d["loss"]), rtol=1e-6)
+    n = 0
+    for pname, p in model.named_parameters():
+        key = "grad__" + pname
+        if key in d:
+            r = d[key]
+            assert p.grad is not None, pname
+            np.testing.assert_allclose(p.grad.cpu().numpy(), r, rtol=1e-4, atol=1e-4 * max(np.abs(r).max(), 1e-12),
+                                       err_msg=pname)
+            n += 1
+        elif p.grad is not None:
+            assert not p.grad.any(), pname
+    assert n > 0
