@@ -30,6 +30,11 @@ SKIP = set(filter(None, os.environ.get("NLDPC_GEN_SKIP", "").split(",")))  # deb
 # kernels, lane 0 of each wave, first 256 workgroups (FusedArgs::stamps, tools/stamps.py)
 STAMPS = os.environ.get("NLDPC_GEN_STAMPS") == "1"
 LDS_BYTES = 160 * 1024 - 2048  # leave room for the compiler / alignment
+
+
+def app_words(N, Z):
+    """32-bit words of one codeword's UCN hard-decision bit array (bit (j, v) = APP[j][v] >= 0)."""
+    return N * ((Z + 31) // 32)
 # check rows up to this degree let the compiler interleave their lane copies (more ILP, more registers)
 CN_PAIR_MAXDC = int(os.environ.get("NLDPC_GEN_CNPAIR", "0"))
 # VN lane copies as packed fp32 pairs (v_pk_add_f32) or all scalar chains.  Measured on gfx950 (stamp
@@ -87,7 +92,7 @@ def auto_geometry(hb, Z):
                     load[int(np.argmin(load))] += d
                 if Q * max(load) > MAX_STATE_REGS:
                     continue
-                cap = (LDS_BYTES // (4 * G) - 32) // Z  # edges per LDS chunk
+                cap = ((LDS_BYTES - 4 * G * app_words(hb.shape[1], Z)) // (4 * G) - 32) // Z  # edges per LDS chunk
                 if cap < int(row_deg.max()):
                     continue
                 nchunks, acc = 1, 0
@@ -132,8 +137,9 @@ class Spec:
         self.d1_cols = balance(single, lambda j: 1, P)  # stateless degree-1 columns
         self.slots = [[e for j in cols_ for e in self.col_edges[j]] for cols_ in self.reg_cols]
         self.smax = max(1, max(len(s) for s in self.slots)) * Q
-        # row chunks: contiguous row ranges whose messages (edges x Z x G) fit in LDS
-        cap = (LDS_BYTES // (4 * G) - 32) // Z
+        # row chunks: contiguous row ranges whose messages (edges x Z x G) fit in LDS beside the UCN bits
+        self.WZ = (Z + 31) // 32
+        cap = ((LDS_BYTES - 4 * G * app_words(self.N, Z)) // (4 * G) - 32) // Z
         self.chunks = []  # (row_begin, row_end, edge_begin, edge_end)
         r0 = 0
         while r0 < self.M:
@@ -294,7 +300,10 @@ def emit(S: Spec) -> str:
             fname = f"post_p{p}" if final else f"vn_p{p}"
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void {fname}({state_params(p)}, {x_params(p)}, const FusedArgs& a, "
-              f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps) {{")
+              f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t* appw, int u, "
+              f"uint32_t d1m, rsrc_t apr) {{")
+            if not final:
+                w("    const bool ucn_ = KIND != NLDPC_NEURAL && a.ucn;  // UCN: hard decisions of the previous posterior")
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
@@ -319,17 +328,32 @@ def emit(S: Spec) -> str:
                     q = 2 * NPAIR + i
                     w("            {")
                     w(f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : xs{i}[{n}];")
+                    w("            float y_;")
                     w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w("                bool m_;")
-                    w(f"                bstore(pr, vo, {X(j, q)}, posterior_m<KIND>(xo_, P_s{i}, a, m_));")
+                    w(f"                y_ = posterior_m<KIND>(xo_, P_s{i}, a, m_);")
+                    w(f"                bstore(pr, vo, {X(j, q)}, y_);")
                     w(f"                bstore8(pm, vm, {X(j, q) // 4}, m_);")
                     w("            } else {")
-                    w(f"                put_post<CM>(pr, vo, {X(j, q)}, posterior<KIND>(xo_, P_s{i}, a), ps);")
+                    w(f"                y_ = posterior<KIND>(xo_, P_s{i}, a);")
+                    w(f"                put_post<CM>(pr, vo, {X(j, q)}, y_, ps);")
                     w("            }")
+                    if not final:
+                        app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xs{i}[{n}], a))"
+                        w(f"            if (ucn_) app_or(appw, {j * S.WZ}, u + {q * ZT}, (it == 0 ? {app0} : y_) >= 0.f);")
                     w("            }")
                 w("        }")
                 w("        __builtin_amdgcn_sched_barrier(0);")
                 s += d
+            if not final and S.d1_cols[p]:
+                # degree-1 columns: their posterior of iteration it-1 was formed in that iteration's read-back
+                # (rd_p), its hard decision kept in d1m
+                w("    if (ucn_) {")
+                for n, j in enumerate(S.d1_cols[p]):
+                    for q in range(Q):
+                        app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xd[{n * Q + q}], a))"
+                        w(f"        app_or(appw, {j * S.WZ}, u + {q * ZT}, it == 0 ? {app0} >= 0.f : ((d1m >> {n * Q + q}) & 1u) != 0u);")
+                w("    }")
             w("}")
 
     # ---------------------------------------------------------------- LDS chunk write / read-back
@@ -367,7 +391,7 @@ def emit(S: Spec) -> str:
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
               f"int u, const FusedArgs& a, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co, "
-              f"uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps) {{")
+              f"uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t& d1m) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
             for q in range(Q):
                 for k, e in mine:
@@ -376,12 +400,15 @@ def emit(S: Spec) -> str:
                 w("    if constexpr (!D1_BYPASS) {")
             for j, e in d1:
                 for q in range(Q):
+                    bit = S.d1_cols[p].index(j) * Q + q
                     w(f"    {{ const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
                     w(f"      const float P_ = fadd(0.f, lds[{own(e, q, e0)}]);")
+                    w("      float y_;")
                     w("      if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
-                    w(f"          bool m_; bstore(pr, vo, {X(j, q)}, posterior_m<KIND>(xo_, P_, a, m_)); "
+                    w(f"          bool m_; y_ = posterior_m<KIND>(xo_, P_, a, m_); bstore(pr, vo, {X(j, q)}, y_); "
                       f"bstore8(pm, vm, {X(j, q) // 4}, m_);")
-                    w(f"      }} else {{ put_post<CM>(pr, vo, {X(j, q)}, posterior<KIND>(xo_, P_, a), ps); }} }}")
+                    w(f"      }} else {{ y_ = posterior<KIND>(xo_, P_, a); put_post<CM>(pr, vo, {X(j, q)}, y_, ps); }}")
+                    w(f"      if (KIND != NLDPC_NEURAL && a.ucn) d1m = (d1m & ~(1u << {bit})) | ((y_ >= 0.f ? 1u : 0u) << {bit}); }}")
             if d1:
                 w("    if (has_co) {  // final message state (last iteration only)")
                 for j, e in d1:
@@ -428,7 +455,8 @@ def emit(S: Spec) -> str:
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void cn_p{p}_c{ci}(float* lds, int u, const FusedArgs& a, int it, "
               f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last, "
-              f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps) {{")
+              f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps, "
+              f"const uint32_t* appw) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
             wo = 0
             for i in S.cn_order[(p, ci)]:
@@ -452,7 +480,17 @@ def emit(S: Spec) -> str:
                               f"else m[{k}] = rq[{k * Z}];")
                         else:
                             w(f"            m[{k}] = rq[{k * Z}];")
-                    w(f"            cn_copy<KIND, {DC}>(m, wv, bv, a, wc, {i});")
+                    w("            float uf_ = 0.f;  // UCN: unsatisfied check (odd number of row variables with APP >= 0)")
+                    w("            if (KIND != NLDPC_NEURAL && a.ucn) {")
+                    w("                uint32_t par_ = 0;")
+                    for k, e in enumerate(es):
+                        c, _ = rot(e, q)
+                        j = int(S.hb_cols[e])
+                        vexpr = f"u + {c}" if c + ZT <= Z else f"u + {c} - (u >= {Z - c} ? {Z} : 0)"
+                        w(f"                {{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZ} + (v_ >> 5)] >> (v_ & 31); }}")
+                    w("                uf_ = (par_ & 1u) ? 1.f : 0.f;")
+                    w("            }")
+                    w(f"            cn_copy<KIND, {DC}>(m, wv, bv, a, wc, {i}, uf_);")
                     for k, e in enumerate(es):
                         if e in d1set:
                             j = int(S.hb_cols[e])
@@ -490,7 +528,7 @@ def emit(S: Spec) -> str:
         nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
         w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
-          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl) {{")
+          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw) {{")
         for i in range(NPAIR):
             w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
         for i in range(NSINGLE):
@@ -549,6 +587,14 @@ def emit(S: Spec) -> str:
                 w(f"        if (a.stamps && blockIdx.x < 256 && (threadIdx.x & 63) == 0) "
                   f"a.stamps[((blockIdx.x * {S.threads // 64} + (threadIdx.x >> 6)) * a.T + it) * 8 + {ph}] = "
                   f"__builtin_amdgcn_s_memtime();")
+        # UCN: the hard-decision bit array of the codewords starts at zero (bits are OR-ed in); every later
+        # iteration's array is cleared in the read-back phase of the iteration before
+        w("    uint32_t d1m = 0;  // UCN: hard decisions of this thread's degree-1 posteriors")
+        w(f"    const rsrc_t apr = make_rsrc(a.app_prev ? a.app_prev + blk * {NZ} : a.xa, a.app_prev ? nlive * {4 * NZ} : 0);")
+        w("    if (KIND != NLDPC_NEURAL && a.ucn) {")
+        w(f"        for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZ}; i_ += {S.threads}) app_all[i_] = 0u;")
+        w("        __syncthreads();")
+        w("    }")
         w("    for (int it = 0; it < a.T; ++it) {")
         stamp(0)
         w("        if (KIND != NLDPC_NEURAL && a.w_vn) {")
@@ -569,7 +615,7 @@ def emit(S: Spec) -> str:
         w("        const uint8_t* pmp = (SAVE && a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t pm = make_rsrc((const float*)(pmp ? pmp + blk * {NZ} : nullptr), pmp ? nlive * {NZ} : 0);")
         if "vn" not in SKIP:
-            w(f"        vn_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, it, pr, vm, xr, pm, ps);")
+            w(f"        vn_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
         w(f"        if constexpr (CNT) {{ if (it >= 1) ps.{cnt_flush}({cnt_slot}, it - 1); else ps.ec = 0; }}")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
@@ -589,7 +635,8 @@ def emit(S: Spec) -> str:
             w(f"        float W{ci}[{nw}], B{ci}[{nw}];")
             w("        {")
             w("            const cfloat_p wc_ = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E) : nullptr;")
-            w("            const cfloat_p bs_ = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E) : nullptr;")
+            w("            const float* bsrc_ = KIND == NLDPC_NEURAL ? a.bias : (a.ucn ? a.w_ucn : nullptr);  // bias / UCN weight")
+            w("            const cfloat_p bs_ = bsrc_ ? (cfloat_p)(bsrc_ + (int64_t)it * E) : nullptr;")
             wo, wl, bl = 0, [], []
             for i in S.cn_order[(p, ci)]:
                 for k, e in enumerate(S.row_edges[i]):
@@ -608,10 +655,14 @@ def emit(S: Spec) -> str:
             stamp(2 + 3 * ci)
             w("        __syncthreads();")
             if "cn" not in SKIP:
-                w(f"        cn_p{p}_c{ci}<KIND, MODE>(lds, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps);")
+                w(f"        cn_p{p}_c{ci}<KIND, MODE>(lds, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw);")
             stamp(3 + 3 * ci)
             w("        __syncthreads();")
-            w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, ps);")
+            w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, ps, d1m);")
+            if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
+                w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
+                w(f"            for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZ}; i_ += {S.threads}) app_all[i_] = 0u;")
+                w("        }")
             stamp(4 + 3 * ci)
             w("        __syncthreads();")
         w("    }")
@@ -619,7 +670,7 @@ def emit(S: Spec) -> str:
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
         w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
-        w(f"    post_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, a.T, lr, vm, xr, lm, ps);")
+        w(f"    post_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr);")
         w(f"    if constexpr (CNT) ps.{cnt_flush}({cnt_slot}, a.T - 1);")
         w("    if (a.c2v_out) {")
         for q in range(Q):
@@ -647,8 +698,10 @@ def emit(S: Spec) -> str:
     w(f"    float* lds = lds_all + g * {CF};")
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
     w(f"    __shared__ int cnt_all[{G * 32}];  // count-only decode: per codeword, two iterations per word")
+    w(f"    __shared__ uint32_t app_all[{G * S.N * S.WZ}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
+    w(f"    uint32_t* appw = app_all + g * {S.N * S.WZ};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
-    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all)", indent="    ")
+    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all, app_all, appw)", indent="    ")
     w("    if constexpr (CNT) {")
     w("        __syncthreads();")
     w("        if (t < a.T) count_iteration(a, cnt_all, nlive, t);")

@@ -267,13 +267,13 @@ static bool fused_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T
     if (disabled || (cfg->flags & NLDPC_FLAG_STREAM)) return false;
     // the SAVE kernels write what the backward needs (QMS: int8 codes, which need an active quantiser)
     if (saving && cfg->kind == NLDPC_QMS && !qms_active(cfg->qbit)) return false;
-    return g->fused >= 0 && !cfg->ucn && !cfg->c2v_in && T <= kFusedMaxT;
+    return g->fused >= 0 && !cfg->c2v_in && T <= kFusedMaxT;
 }
 
 static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
-                         const float* w_cn, const float* bias, const float* w_vn, float* const* outs, float* c2v,
-                         void* saved, hipStream_t s, const uint8_t* cnt_y = nullptr, int32_t cnt_conv = 0,
-                         int64_t* counts = nullptr) {
+                         const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
+                         float* const* outs, const float* app_prev, float* c2v, void* saved, hipStream_t s,
+                         const uint8_t* cnt_y = nullptr, int32_t cnt_conv = 0, int64_t* counts = nullptr) {
     int n = 0;
     const FusedSpec& f = fused_specs(&n)[g->fused];
     FusedArgs fa{};
@@ -283,6 +283,10 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     fa.xa = xa;
     fa.w_cn = w_cn;
     fa.bias = bias;
+    fa.ucn = cfg->ucn ? 1 : 0;
+    fa.w_ucn = cfg->ucn ? w_ucn : nullptr;
+    fa.first_iter = cfg->first_iter;
+    fa.app_prev = (cfg->ucn && cfg->first_iter > 0) ? app_prev : nullptr;
     fa.w_vn = cfg->vn_cumulative ? w_vn : nullptr;
     fa.vn_prefix = cfg->vn_prefix;
     fa.sp_plan = g->dev.sp_plan;
@@ -380,7 +384,7 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
     if (fused) {
         if (!c2v && !(cfg->flags & NLDPC_FLAG_NO_STATE))
             return fail(NLDPC_EINVAL, "nldpc_forward: c2v is required unless NLDPC_FLAG_NO_STATE");
-        return fused_forward(g, cfg, B, T, xa, w_cn, bias, w_vn, outs, c2v, saved, s);
+        return fused_forward(g, cfg, B, T, xa, w_cn, w_ucn, bias, w_vn, outs, app_prev, c2v, saved, s);
     }
     if (!c2v) return fail(NLDPC_EINVAL, "nldpc_forward: c2v is required by the streaming path");
     if (!v2c && !saved) return fail(NLDPC_EINVAL, "nldpc_forward: need v2c scratch or saved buffer");
@@ -457,13 +461,12 @@ extern "C" int nldpc_forward_count(const nldpc_graph* g, const nldpc_cfg* cfg, i
     if (cfg->kind == NLDPC_NEURAL && (!w_cn || !bias))
         return fail(NLDPC_EINVAL, "nldpc_forward_count: the Neural decoder needs w_cn and bias");
     if (cfg->vn_cumulative && !w_vn) return fail(NLDPC_EINVAL, "nldpc_forward_count: vn_cumulative needs w_vn");
-    (void)w_ucn;
-    if (!fused_eligible(g, cfg, T, false))
+    if (!fused_eligible(g, cfg, T, false) || (cfg->ucn && cfg->first_iter > 0))
         return fail(NLDPC_EUNSUPPORTED, "nldpc_forward_count: needs the fused path (a compiled base graph, no UCN, "
                                         "fresh state, T <= 64); use nldpc_forward + nldpc_ber_count instead");
     DeviceGuard guard(g->device);
     nldpc_cfg c = *cfg;
     c.flags |= NLDPC_FLAG_NO_STATE;
-    return fused_forward(g, &c, B, T, xa, w_cn, bias, w_vn, nullptr, nullptr, nullptr, static_cast<hipStream_t>(stream),
-                         y, convention, counts);
+    return fused_forward(g, &c, B, T, xa, w_cn, w_ucn, bias, w_vn, nullptr, nullptr, nullptr, nullptr,
+                         static_cast<hipStream_t>(stream), y, convention, counts);
 }

@@ -19,6 +19,9 @@ struct FusedArgs {
     const float* xa;     // [B][N][Z]
     const float* w_cn;   // [T][E] or nullptr
     const float* bias;   // [T][E] or nullptr
+    const float* w_ucn;  // [T][E] UCN weights (ucn), or nullptr
+    const float* app_prev;  // [B][N][Z] posterior of iteration first_iter-1 (UCN, first_iter > 0), or nullptr
+    int32_t ucn, first_iter;
     const float* w_vn;   // [vn_prefix + T][N] or nullptr
     int32_t vn_prefix;
     float lo, hi;
@@ -116,6 +119,13 @@ template <int KIND>
 __device__ __forceinline__ f2 chan2(f2 x, const FusedArgs& a) {
     if (KIND == NLDPC_NEURAL) return x;
     return f2{chan<KIND>(x.x, a), chan<KIND>(x.y, a)};
+}
+
+// UCN hard-decision exchange (Boosted…py:339-374): the owner of variable copy v of column j ORs the bit
+// APP[j][v] >= 0 into the codeword's LDS bit array (word base + v / 32); the check node of copy h reads
+// the bits of its row's variables at (h + s_e) mod Z and takes their parity (odd = unsatisfied).
+__device__ __forceinline__ void app_or(uint32_t* appw, int base, int v, bool bit) {
+    if (bit) atomicOr(appw + base + (v >> 5), 1u << (v & 31));
 }
 
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
@@ -273,7 +283,7 @@ __device__ __forceinline__ void PostSink::flush_wave(int* cntl, int it) {
 // only, which no sum of the decoder can observe).  ~19 VALU per edge copy instead of ~45.
 template <int DC, int KIND>
 __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC], bool has_w, int qbit, float lo,
-                                            float hi) {
+                                            float hi, bool ucn, float uf, const float (&wu)[DC]) {
     constexpr uint32_t kInit = 0x461C4000u << 1;  // key of 10000.f
     uint32_t min1 = kInit, min2 = kInit;
     uint32_t key[DC];
@@ -307,7 +317,11 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
     for (int k = 0; k < DC; ++k) {
         const bool sel = key[k] == min1;
         const float mag = sel ? mg2 : mg1;
-        const float x2 = relu_mask(has_w ? fmul(mag, w[k]) : mag);
+        // with UCN: (|x| w_cn)(1 - u) + (|x| w_ucn) u, the reference's arithmetic (Boosted…py:436-488)
+        const float x1 = !has_w ? mag
+                         : (ucn ? fadd(fmul(fmul(mag, w[k]), fadd(-uf, 1.f)), fmul(fmul(mag, wu[k]), uf))
+                                : fmul(mag, w[k]));
+        const float x2 = relu_mask(x1);
         const float x3 = KIND == NLDPC_QMS ? quantize_active(x2, qbit) : __builtin_amdgcn_fmed3f(x2, lo, hi);
         const bool neg = KIND == NLDPC_MS && (sel ? n2 : n1);
         m[k] = ((par != pos[k]) != neg) ? x3 : -x3;
@@ -316,19 +330,26 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
 
 // check node of one check copy in place (m: gathered v2c -> c2v), every kind: Neural through the
 // specialised neural_row, MS / QMS through boosted_row, SP through the shared cn_core + cn_epilogue
+// bv: Neural biases, or (Boosted with UCN) the UCN weights; uf: the copy's UCN flag
 template <int KIND, int DC>
 __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], const float (&bv)[DC],
-                                        const FusedArgs& a, bool has_w, int row) {
+                                        const FusedArgs& a, bool has_w, int row, float uf) {
     if constexpr (KIND == NLDPC_NEURAL) {
         neural_row<DC>(m, wv, bv);
     } else if (KIND == NLDPC_MS || (KIND == NLDPC_QMS && qms_active_q(a.qbit))) {
-        boosted_row<DC, KIND>(m, wv, has_w, a.qbit, a.lo, a.hi);
+        boosted_row<DC, KIND>(m, wv, has_w, a.qbit, a.lo, a.hi, a.ucn != 0, uf, bv);
     } else {
         CnCore<DC> core;
         cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core, SpRow{a.sp_plan + row * kSpPlanBytes, a.tanh});
+        if (a.ucn) {
 #pragma unroll
-        for (int k = 0; k < DC; ++k)
-            m[k] = cn_epilogue<KIND, false>(core.out0[k], wv[k], 0.f, 0.f, 0.f, has_w, false, a.qbit, a.lo, a.hi).c;
+            for (int k = 0; k < DC; ++k)
+                m[k] = cn_epilogue<KIND, true>(core.out0[k], wv[k], bv[k], 0.f, uf, has_w, true, a.qbit, a.lo, a.hi).c;
+        } else {
+#pragma unroll
+            for (int k = 0; k < DC; ++k)
+                m[k] = cn_epilogue<KIND, false>(core.out0[k], wv[k], 0.f, 0.f, 0.f, has_w, false, a.qbit, a.lo, a.hi).c;
+        }
     }
 }
 

@@ -155,9 +155,9 @@ def test_fast_path_selection():
     from nldpc import _lib
     from nldpc.decode import KIND_NEURAL, DecodeCfg
     L = _lib.lib()
-    for bg, Z, want in ((BG2, 384, 1), (BG2, 16, 1), (WIMAX, 24, 1), (BG2, 64, 0)):
+    for bg, Z, want in ((BG2, 384, 1), (BG2, 16, 1), (WIMAX, 24, 1), (BG2, 96, 1), (BG2, 64, 0), (BG2, 104, 0)):
         g = _graph(bg, Z)
-        for save, ucn, exp in ((0, False, want), (1, False, want), (0, True, 0)):
+        for save, ucn, exp in ((0, False, want), (1, False, want), (0, True, want)):
             cfg = DecodeCfg(KIND_NEURAL if not ucn else 1, ucn=ucn).c_struct(False)
             out = ctypes.c_int32(-1)
             _lib.check(L.nldpc_fast_path(g.handle(DEV), ctypes.byref(cfg), 4, 20, save, ctypes.byref(out)))
@@ -265,8 +265,8 @@ def test_count_only_decode_equals_decode_then_count(bg, Z, B, kind):
     decode(g, fast, x, 1, **{k: v[:1] for k, v in kw.items()})  # this configuration is on the fused path
 
 
-def test_count_only_decode_ucn_falls_back():
-    """Configurations outside the fused path (UCN) are counted by decode + the device counter."""
+def test_count_only_decode_ucn():
+    """UCN configurations are counted inside the fused kernel too (counts == decode + counter)."""
     from nldpc.channel import ber_counts
     from nldpc.decode import KIND_MS, DecodeCfg, decode, decode_count
     g = _graph(BG2, 16)
@@ -277,3 +277,85 @@ def test_count_only_decode_ucn_falls_back():
     cfg = DecodeCfg(kind=KIND_MS, ucn=True)
     outs, _, _ = decode(g, cfg, x, T, w_cn=w, w_ucn=w * 0.5)
     assert torch.equal(decode_count(g, cfg, x, T, w_cn=w, w_ucn=w * 0.5), ber_counts(list(outs)))
+
+
+UCN_FIXTURES = [n for n in BOOSTED if any(t in n for t in ("nw112", "nw223", "nw330", "nw333")) and "wimax" not in n
+                or n == "boosted_wimax_z24_qms5_nw112" or n == "boosted_wimax_z24_ms_nw333"]
+
+
+@pytest.mark.parametrize("name", UCN_FIXTURES)
+def test_ucn_fixtures_on_fused_path(golden, name):
+    """UCN (unsatisfied-check weighting, Boosted…py:339-374) on the register-resident kernel, required
+    with path="fused": the hard decisions of the previous posterior go through an LDS bit array."""
+    from nldpc.decode import DecodeCfg, decode
+    d = golden(name)
+    g = _graph(_bg(name), int(d["Z"]))
+    T = int(d["T"])
+    nw = tuple(int(v) for v in d["nw"])
+    w_cn, w_ucn, w_vn, use_ucn = boosted_params(d, g, T, nw, [])
+    if not use_ucn:
+        pytest.skip("UCN weights unused for this sharing combination")
+    kind, q = int(d["dtype"]), int(d["q"])
+    cfg = DecodeCfg(kind=kind, qbit=q, ucn=True, vn_cumulative=w_vn is not None, path="fused")
+    outs, _, _ = decode(g, cfg, torch.from_numpy(d["x"]).to(DEV), T, w_cn=w_cn, w_ucn=w_ucn, w_vn=w_vn)
+    o, ref = outs.cpu().numpy(), d["outputs"][:T]
+    if kind == 0:
+        sp_check(o, ref)
+    else:
+        assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} soft values differ"
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("Z,B", [(384, 2), (16, 19)])
+def test_ucn_fused_equals_stream_later_segment(kind, Z, B):
+    """A UCN segment that starts at iteration 3 of a forward (first_iter > 0, the previous posterior
+    given as app_prev) with per-check CN / UCN weights and cumulative VN weights: fused == streaming,
+    outputs and final message state, also when saving for the backward."""
+    from nldpc.decode import DecodeCfg, decode
+    T = 4
+    g = _graph(BG2, Z)
+    gen = torch.Generator().manual_seed(31 * kind + Z)
+    x = (2 * (-1 + 0.9 * torch.randn(B, 52, Z, generator=gen)) / 0.81).float().to(DEV)
+    app = (3 * torch.randn(B, 52 * Z, generator=gen)).to(DEV)
+    w_cn = (0.5 + torch.rand(T, 42, generator=gen))[:, torch.as_tensor(g.chk)].contiguous().to(DEV)
+    w_ucn = (0.2 + torch.rand(T, 42, generator=gen))[:, torch.as_tensor(g.chk)].contiguous().to(DEV)
+    w_vn = (0.8 + 0.4 * torch.rand(T + 3, 52, generator=gen)).to(DEV)
+    for save in (False, True):
+        res = {}
+        for path in ("stream", "fused"):
+            cfg = DecodeCfg(kind=kind, qbit=5, ucn=True, vn_cumulative=True, first_iter=3, vn_prefix=3, path=path)
+            res[path] = decode(g, cfg, x, T, w_cn=w_cn, w_ucn=w_ucn, w_vn=w_vn, app_prev=app, save=save)
+        assert torch.equal(res["stream"][0], res["fused"][0])
+        assert torch.equal(res["stream"][1], res["fused"][1])
+
+
+@pytest.mark.parametrize("kind", [3, 2, 1])
+def test_lifting_96_fused_matches_oracle(kind):
+    """A lifting size beyond the hand-listed ones (BG2 z=96: geometry chosen by gen_fused.auto_geometry,
+    2 codewords x 5 parts x 96 lanes per workgroup, one LDS chunk) decodes on the register-resident
+    kernel (path="fused" is required) bit-exactly against the CPU oracle."""
+    from nldpc.decode import DecodeCfg, decode
+    from oracle.ldpc_oracle import OracleGraph, boosted_forward, neural_forward, quantize
+    T, B, Z = 6, 5, 96
+    g = _graph(BG2, Z)
+    og = OracleGraph(BG2, Z)
+    gen = torch.Generator().manual_seed(96 + kind)
+    x = (2 * (-1 + 0.85 * torch.randn(B, 52, Z, generator=gen)) / 0.7225).float()
+    if kind == 3:
+        w = torch.rand(T, g.E, generator=gen) * 1.2
+        b = torch.randn(T, g.E, generator=gen) * 0.1
+        outs, _, _ = decode(g, DecodeCfg(kind, path="fused"), x.to(DEV), T, w_cn=w.to(DEV), bias=b.to(DEV))
+        ref = torch.stack(neural_forward(og, x, list(w), list(b))).numpy()
+    else:
+        if kind == 2:
+            x = quantize(x, 5)
+        wc = 0.5 + torch.rand(T, 42, generator=gen)
+        wv = 0.8 + 0.4 * torch.rand(T, 52, generator=gen)
+        cfg = DecodeCfg(kind, qbit=5, vn_cumulative=True, path="fused")
+        outs, _, _ = decode(g, cfg, x.to(DEV), T, w_cn=wc[:, torch.as_tensor(g.chk)].contiguous().to(DEV),
+                            w_vn=wv.to(DEV))
+        r = boosted_forward(og, x, dtype=kind, q=5, nw=(2, 0, 2), iters=list(range(T)), w_cn=lambda t: wc[t],
+                            w_ucn=lambda t: None, w_vn=lambda t: wv[t])
+        ref = torch.stack([r[t] for t in range(T)]).numpy()
+    o = outs.cpu().numpy()
+    assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} differ"
