@@ -2,7 +2,7 @@
 
     python bench.py [--gpus N --steps K --warmup W]            # N>1: starts N rank processes itself
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
-    python bench.py --workload cfg2|cfg5                       # the other GPU configs (own lines)
+    python bench.py --workload cfg2|cfg5|cfg3ucn               # the other GPU configs (own lines)
 
 Default workload cfg3: a step = one NeuralLDPCDecoder.forward over the rank's batch of B codewords
 (default 65536 per GPU, weak scaling), T=20 iterations, every iteration's posterior written (the
@@ -47,6 +47,8 @@ WORKLOADS = {
     "cfg3": ("basegraph2_set0.txt", 384, 20, 65536),
     "cfg2": ("wman_N0576_R34_z24.txt", 24, 20, 4096),
     "cfg5": ("basegraph2_set0.txt", 384, 50, 2048),
+    # side line (not a BASELINE config): cfg3's decode with the Boosted MS decoder and UCN on
+    "cfg3ucn": ("basegraph2_set0.txt", 384, 20, 65536),
 }
 
 
@@ -275,10 +277,24 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
     from nldpc.channel import awgn_llr, ber_counts, sigma_for
 
     M, N = bg.shape
-    conn = nd.ConnectingMatrixTorch(nd.ConnectingMatrix(Z, bg), device=dev)
-    model = nd.NeuralLDPCDecoder(T, B, conn).to(dev)  # reference default parameters: w = 0.5, b = 0
+    ucn = args.workload == "cfg3ucn"
+    if ucn:  # Boosted MS, NW(1,1,2): per-edge CN and UCN weights, per-column VN weights (fused UCN kernel)
+        from boosted_neural_ldpc_decoder.BoostedNeuralLDPCDecoder import BoostedNeuralLDPCDecoder
+        from boosted_neural_ldpc_decoder.ConnectingMatrix import ConnectingMatrix
+        from boosted_neural_ldpc_decoder.ConnectingMatrixTorch import ConnectingMatrixTorch
+        from boosted_neural_ldpc_decoder.struct.DecoderType import DecoderType
+        from boosted_neural_ldpc_decoder.struct.NodeWeightSharingConfig import NodeWeightSharingConfig
+        from nldpc.channel import boosted_code_rate
+        conn = ConnectingMatrixTorch(ConnectingMatrix(Z, bg), device=dev)
+        model = BoostedNeuralLDPCDecoder(T, B, conn, node_weight_sharing_config=NodeWeightSharingConfig(1, 1, 2),
+                                         decoding_type=DecoderType.MS).to(dev)
+        model.eval()
+        rate = boosted_code_rate(N, M)
+    else:
+        conn = nd.ConnectingMatrixTorch(nd.ConnectingMatrix(Z, bg), device=dev)
+        model = nd.NeuralLDPCDecoder(T, B, conn).to(dev)  # reference default parameters: w = 0.5, b = 0
+        rate = (N - M) / (N - 2)  # reference code-rate formula (AWGNPassedDatagen.py:47 / neural :36)
     E = int(conn.sum_edge)
-    rate = (N - M) / (N - 2)  # reference code-rate formula (AWGNPassedDatagen.py:47 / neural :36)
     offset, _ = nd_dist.shard(world * B, rank, world)  # weak scaling: rank r holds [r*B, (r+1)*B)
     xa = awgn_llr(B, N, Z, sigma_for(args.ebn0, rate), seed=2042, b_offset=offset, device=dev)
     xa_host = xa[:min(B, 2048)].cpu()  # the CPU baseline decodes these same Philox codewords
@@ -332,8 +348,10 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
     if rank != 0:
         return None
     bits_total = world * B * N * Z
-    tag = {"cfg3": "bg2_z384", "cfg2": "wimax_z24"}.get(args.workload, f"z{Z}")
+    tag = {"cfg3": "bg2_z384", "cfg3ucn": "bg2_z384", "cfg2": "wimax_z24"}.get(args.workload, f"z{Z}")
     wl = {"cfg3": f"cfg3 Neural BG2 set0 z={Z}, T={T}, all T posteriors written",
+          "cfg3ucn": f"cfg3 decode with BoostedNeuralLDPCDecoder MS NW(1,1,2) (UCN on), BG2 set0 z={Z}, T={T}, "
+                     "all T posteriors written",
           "cfg2": f"cfg2 Neural WiMAX N=576 R=3/4 z={Z}, T={T}, all T posteriors written"}[args.workload]
     res = {
         "metric": METRIC,
@@ -350,8 +368,8 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic: all-zero codewords, BPSK/AWGN Eb/N0={args.ebn0} dB, on-device Philox; "
-                "reference default weights (w=0.5, b=0)",
-        "config": {"workload": wl, "model": "NeuralLDPCDecoder", "global_batch": world * B, "per_gpu_batch": B,
+                + ("reference init weights (1.0)" if ucn else "reference default weights (w=0.5, b=0)"),
+        "config": {"workload": wl, "model": "BoostedNeuralLDPCDecoder" if ucn else "NeuralLDPCDecoder", "global_batch": world * B, "per_gpu_batch": B,
                    "seq_len": N * Z, "iters": T, "parallelism": f"dp{world}"},
         "ber": {"ebn0_db": args.ebn0, "ber_last_iter": float(counts[-1, 0]) / bits_total,
                 "fer_last_iter": float(counts[-1, 1]) / (world * B),
@@ -373,7 +391,7 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
     if prof is not None:
         res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T), args.steps, B, Z, world, tag,
                                    4 * (2 * T * E * Z + (T + 1) * N * Z), ceilings, f"{args.workload}_B{B}")
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and not ucn:
         res["cpu_baseline"] = cpu_baseline(bg, Z, T, xa_host, gpu_last, args.cpu_seconds)
     return res
 

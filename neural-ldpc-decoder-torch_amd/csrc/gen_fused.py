@@ -44,6 +44,15 @@ PACK_VN = os.environ.get("NLDPC_GEN_PACK") == "1"
 # experiment knob: no opaque row base in the check-node phase (lets the compiler prove the row copies'
 # LDS slots disjoint and overlap them, at its own register cost)
 NORO = os.environ.get("NLDPC_GEN_NORO") == "1"
+# Forward chunk schedule.  0: one LDS image of a row chunk at a time, write | check nodes | read-back
+# separated by barriers (every phase is either LDS traffic or VALU work).  1: two LDS buffers of
+# smaller chunks, software-pipelined so that each phase mixes one chunk's check nodes with another
+# chunk's owner writes or read-backs: [VN, W0] [CN0, W1] [R0, CN1] [W2, R1] [CN2, W3] [R2, CN3] ...
+# Default 1 (with CNPIPE: cfg3 kernel 55.2 ms against 58.7 ms for 0/0, tools/gpu_ab.sh, r2)
+PIPE = os.environ.get("NLDPC_GEN_PIPE", "1") == "1"
+# Check-node phase: 1 = software-pipelined row copies (the LDS reads of the next row copy are issued
+# before the current one computes, so the LDS latency hides behind arithmetic instead of stalling)
+CNPIPE = os.environ.get("NLDPC_GEN_CNPIPE", "1") == "1"
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
 # chosen by auto_geometry
@@ -120,9 +129,10 @@ def balance(items, weight, P):
 
 
 class Spec:
-    def __init__(self, tag, hb, Z, G, P, Q):
+    def __init__(self, tag, hb, Z, G, P, Q, pipe=False):
         assert Z % Q == 0
         self.tag, self.hb, self.Z, self.G, self.P, self.Q = tag, hb, Z, G, P, Q
+        self.pipe = pipe
         self.ZT = Z // Q
         self.M, self.N = hb.shape
         rows, cols = np.nonzero(hb != -1)
@@ -140,6 +150,8 @@ class Spec:
         # row chunks: contiguous row ranges whose messages (edges x Z x G) fit in LDS beside the UCN bits
         self.WZ = (Z + 31) // 32
         cap = ((LDS_BYTES - 4 * G * app_words(self.N, Z)) // (4 * G) - 32) // Z
+        if pipe:  # two buffers; only the count-only counters (G*128 B) share the remaining KiB
+            cap = ((160 * 1024 - 1024 - 4 * G * app_words(self.N, Z)) // (8 * G) - (32 if G > 1 else 0)) // Z
         self.chunks = []  # (row_begin, row_end, edge_begin, edge_end)
         r0 = 0
         while r0 < self.M:
@@ -154,6 +166,7 @@ class Spec:
         self.chunk_floats = max(e1 - e0 for _, _, e0, e1 in self.chunks) * Z
         if G > 1:  # codeword stride = 1 (mod 32 banks) so lanes of different codewords do not collide
             self.chunk_floats += (1 - self.chunk_floats) % 32
+        self.nbuf = 2 if pipe else 1
         self.cn_rows = [balance(list(range(r0, r1)), lambda i: len(self.row_edges[i]), P)
                         for (r0, r1, _, _) in self.chunks]
         self.lanes = G * self.ZT  # threads per part
@@ -458,55 +471,85 @@ def emit(S: Spec) -> str:
               f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps, "
               f"const uint32_t* appw) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
-            wo = 0
+            # row copies in order; weight offsets of each row in the preloaded W/Bv arrays
+            rcs, woff, wo = [], {}, 0
             for i in S.cn_order[(p, ci)]:
+                woff[i] = wo
+                wo += len(S.row_edges[i])
+                for q in range(Q):
+                    rcs.append((i, q))
+
+            def rc_load(n):
+                i, q = rcs[n]
                 es = S.row_edges[i]
                 DC, e0 = len(es), es[0]
-                w(f"    {{  // check row {i}: edges {e0}..{e0 + DC - 1}; weights preloaded (W/Bv[{wo}..])")
-                w(f"        float wv[{DC}], bv[{DC}];")
-                w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{wo} + k]; bv[k] = Bv[{wo} + k]; }}")
-                w("        const bool wc = a.w_cn != nullptr;")
-                wo += DC
-                for q in range(Q):
-                    w("        {  // one check copy at a time: the state owns the registers")
-                    w(f"            float m[{DC}];")
-                    w(f"            int ro = {(e0 - e0c) * Z + q * ZT} + u;  // one base VGPR per row copy: the edges ride in")
-                    if not NORO:
-                        w("            asm volatile(\"\" : \"+v\"(ro));  // the 16-bit DS offset")
-                    w("            float* rq = lds + ro;")
-                    for k, e in enumerate(es):
-                        if e in d1set:
-                            w(f"            if constexpr (D1_BYPASS) m[{k}] = cd[{S.cd_index[p].index((e, q))}]; "
-                              f"else m[{k}] = rq[{k * Z}];")
-                        else:
-                            w(f"            m[{k}] = rq[{k * Z}];")
-                    w("            float uf_ = 0.f;  // UCN: unsatisfied check (odd number of row variables with APP >= 0)")
-                    w("            if (KIND != NLDPC_NEURAL && a.ucn) {")
-                    w("                uint32_t par_ = 0;")
-                    for k, e in enumerate(es):
-                        c, _ = rot(e, q)
-                        j = int(S.hb_cols[e])
-                        vexpr = f"u + {c}" if c + ZT <= Z else f"u + {c} - (u >= {Z - c} ? {Z} : 0)"
-                        w(f"                {{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZ} + (v_ >> 5)] >> (v_ & 31); }}")
-                    w("                uf_ = (par_ & 1u) ? 1.f : 0.f;")
-                    w("            }")
-                    w(f"            cn_copy<KIND, {DC}>(m, wv, bv, a, wc, {i}, uf_);")
-                    for k, e in enumerate(es):
-                        if e in d1set:
-                            j = int(S.hb_cols[e])
-                            c, dv = rot(e, q)
-                            w("            if constexpr (D1_BYPASS) {")
-                            w(f"                const uint32_t dv_ = {dv};")
-                            w(f"                put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, "
-                              f"fadd(cd[{S.cd_index[p].index((e, q))}], fadd(0.f, m[{k}])), ps);")
-                            w(f"                if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m[{k}]);")
-                            w(f"            }} else {{ rq[{k * Z}] = m[{k}]; }}")
-                        else:
-                            w(f"            rq[{k * Z}] = m[{k}];")
-                    w("        }")
-                    if Q > 1 and DC > CN_PAIR_MAXDC:
-                        w("        __builtin_amdgcn_sched_barrier(0);")
+                w(f"    float m{n}[{DC}];  // row {i} copy {q}")
+                w(f"    float* rq{n};")
+                w("    {")
+                w(f"        int ro = {(e0 - e0c) * Z + q * ZT} + u;  // one base VGPR per row copy: the edges ride in")
+                if not NORO:
+                    w("        asm volatile(\"\" : \"+v\"(ro));  // the 16-bit DS offset")
+                w(f"        rq{n} = lds + ro;")
                 w("    }")
+                for k, e in enumerate(es):
+                    if e in d1set:
+                        w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = cd[{S.cd_index[p].index((e, q))}]; "
+                          f"else m{n}[{k}] = rq{n}[{k * Z}];")
+                    else:
+                        w(f"    m{n}[{k}] = rq{n}[{k * Z}];")
+
+            def rc_compute(n):
+                i, q = rcs[n]
+                es = S.row_edges[i]
+                DC = len(es)
+                w("    {")
+                w(f"        float wv[{DC}], bv[{DC}];")
+                w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{woff[i]} + k]; bv[k] = Bv[{woff[i]} + k]; }}")
+                w("        const bool wc = a.w_cn != nullptr;")
+                w("        float uf_ = 0.f;  // UCN: unsatisfied check (odd number of row variables with APP >= 0)")
+                w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
+                w("            uint32_t par_ = 0;")
+                for k, e in enumerate(es):
+                    c, _ = rot(e, q)
+                    j = int(S.hb_cols[e])
+                    vexpr = f"u + {c}" if c + ZT <= Z else f"u + {c} - (u >= {Z - c} ? {Z} : 0)"
+                    w(f"            {{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZ} + (v_ >> 5)] >> (v_ & 31); }}")
+                w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
+                w("        }")
+                if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
+                    w(f"        cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
+                for k, e in enumerate(es):
+                    if e in d1set:
+                        j = int(S.hb_cols[e])
+                        c, dv = rot(e, q)
+                        w("        if constexpr (D1_BYPASS) {")
+                        w(f"            const uint32_t dv_ = {dv};")
+                        w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, "
+                          f"fadd(cd[{S.cd_index[p].index((e, q))}], fadd(0.f, m{n}[{k}])), ps);")
+                        w(f"            if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m{n}[{k}]);")
+                        w(f"        }} else {{ rq{n}[{k * Z}] = m{n}[{k}]; }}")
+                    elif "cnwrite" in SKIP:  # (timing experiment: keep the value live without the LDS write)
+                        w(f"        asm volatile(\"\" :: \"v\"(m{n}[{k}]));")
+                    else:
+                        w(f"        rq{n}[{k * Z}] = m{n}[{k}];")
+                w("    }")
+
+            if CNPIPE:
+                # the next row copy's reads go out before this one computes (its slots are disjoint from
+                # every slot this one writes, so program order already allows it)
+                if rcs:
+                    rc_load(0)
+                for n in range(len(rcs)):
+                    if n + 1 < len(rcs):
+                        rc_load(n + 1)
+                    w("    __builtin_amdgcn_sched_barrier(0);")
+                    rc_compute(n)
+            else:
+                for n in range(len(rcs)):
+                    rc_load(n)
+                    rc_compute(n)
+                    if Q > 1 and len(S.row_edges[rcs[n][0]]) > CN_PAIR_MAXDC:
+                        w("    __builtin_amdgcn_sched_barrier(0);")
             w("}")
 
     # ---------------------------------------------------------------- the kernel
@@ -557,7 +600,8 @@ def emit(S: Spec) -> str:
         w("    if constexpr (D1_BYPASS) {")
         for idx, (e, q) in enumerate(S.cd_index[p]):
             c, dv = rot(e, q)
-            w(f"        cd[{idx}] = bload(xr, vo + {dv}, {4 * (int(S.hb_cols[e]) * Z + c)});")
+            # (0 + xa): the v2c of a degree-1 edge, canonical (never -0), as the check node sees it
+            w(f"        cd[{idx}] = fadd(0.f, bload(xr, vo + {dv}, {4 * (int(S.hb_cols[e]) * Z + c)}));")
         w("    } else {")
         w(f"        for (int k = 0; k < {ncd}; ++k) cd[k] = 0.f;")
         w("    }")
@@ -628,10 +672,10 @@ def emit(S: Spec) -> str:
           f"svp ? nlive * {S.E * Z} * SB : 0);")
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
         stamp(1)
-        for ci in range(len(S.chunks)):
+        def preload(ci):
             nw = S.cn_nw[(p, ci)]
-            # this chunk's check-node weights, by whole-row scalar loads issued before the write phase
-            # (their latency overlaps the LDS writes and the barrier, not the check rows' LDS waits)
+            # this chunk's check-node weights, by whole-row scalar loads issued a phase ahead of its check
+            # nodes (their latency overlaps LDS traffic and a barrier, not the check rows' LDS waits)
             w(f"        float W{ci}[{nw}], B{ci}[{nw}];")
             w("        {")
             w("            const cfloat_p wc_ = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E) : nullptr;")
@@ -651,20 +695,62 @@ def emit(S: Spec) -> str:
                 w(f"            if (KIND == NLDPC_NEURAL || bs_) {{ {' '.join(bl)} }}")
                 w(f"            else {{ for (int k = 0; k < {nw}; ++k) B{ci}[k] = 0.f; }}")
             w("        }")
-            w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, lds, u, a, it, sv, vc);")
-            stamp(2 + 3 * ci)
-            w("        __syncthreads();")
+
+        def buf(ci):
+            return f"lds + {(ci % S.nbuf) * CF}" if S.nbuf > 1 else "lds"
+
+        def op_w(ci):
+            preload(ci)
+            w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, {buf(ci)}, u, a, it, sv, vc);")
+
+        def op_cn(ci):
             if "cn" not in SKIP:
-                w(f"        cn_p{p}_c{ci}<KIND, MODE>(lds, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw);")
-            stamp(3 + 3 * ci)
-            w("        __syncthreads();")
-            w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, lds, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, ps, d1m);")
+                w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw);")
+
+        def op_r(ci):
+            w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
+              f"ps, d1m);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
                 w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
                 w(f"            for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZ}; i_ += {S.threads}) app_all[i_] = 0u;")
                 w("        }")
-            stamp(4 + 3 * ci)
-            w("        __syncthreads();")
+
+        K = len(S.chunks)
+        if not S.pipe:
+            for ci in range(K):
+                op_w(ci)
+                stamp(2 + 3 * ci)
+                w("        __syncthreads();")
+                op_cn(ci)
+                stamp(3 + 3 * ci)
+                w("        __syncthreads();")
+                op_r(ci)
+                stamp(4 + 3 * ci)
+                w("        __syncthreads();")
+        else:
+            # phases: [W0] | [CN0, W1] | [R0, CN1] | [W2, R1] | [CN2, W3] | [R2, CN3] | ... | [R_{K-1}] (the last
+            # read-back runs into the next iteration's VN and W0, whose buffer was last read two phases back).
+            # W_c reuses the buffer of chunk c-2, read (R_{c-2}) a phase earlier.
+            phases = [[("w", 0)]]
+            c = 0
+            while c < K:
+                phases.append([("cn", c)] + ([("w", c + 1)] if c + 1 < K else []))
+                phases.append([("r", c)] + ([("cn", c + 1)] if c + 1 < K else []))
+                if c + 1 < K:
+                    phases.append(([("w", c + 2)] if c + 2 < K else []) + [("r", c + 1)])
+                c += 2
+            # phase dependencies hold: each W_c is after R_{c-2}'s phase, each CN_c after W_c's, each R_c after CN_c's
+            for k, ph in enumerate(phases):
+                for kind_, ci in ph:
+                    {"w": op_w, "cn": op_cn, "r": op_r}[kind_](ci)
+                if k < len(phases) - 1:
+                    w("        __syncthreads();")
+            # a K-odd schedule ends with [R_{K-1}] alone after [R_{K-2}... ]: the next W0 (buffer 0) follows
+            # R_{K-1} (buffer 0) in other waves -> keep a barrier; K even: R_{K-1} reads buffer 1
+            if K % 2 == 1:
+                w("        __syncthreads();")
+            else:  # UCN: the hard-decision bits cleared in R_{K-1} must be clear before any wave's next VN
+                w("        if (KIND != NLDPC_NEURAL && a.ucn) __syncthreads();")
         w("    }")
         w("    const float* pl = a.outs.p[a.T - 1];")
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
@@ -680,7 +766,7 @@ def emit(S: Spec) -> str:
         w("}")
     w("template <int KIND, int MODE>")
     w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void kernel(FusedArgs a) {{")
-    w(f"    __shared__ float lds_all[{CF * G}];")
+    w(f"    __shared__ float lds_all[{CF * G * S.nbuf}];")
     w("    const int t = threadIdx.x;")
     w(f"    // every wave lies in one part ({S.lanes} threads per part): the part is wave-uniform")
     w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes});")
@@ -695,7 +781,7 @@ def emit(S: Spec) -> str:
     w(f"    const uint32_t vc = g < nlive ? 4u * (g * {S.E * Z} + u) : 0x80000000u;  // [E][Z] c2v state")
     w(f"    const rsrc_t xr = make_rsrc(a.xa + blk * {NZ}, nlive * {4 * NZ});")
     w(f"    const rsrc_t cr = make_rsrc(a.c2v_out ? a.c2v_out + blk * {S.E * Z} : a.xa, nlive * {4 * S.E * Z});")
-    w(f"    float* lds = lds_all + g * {CF};")
+    w(f"    float* lds = lds_all + g * {CF * S.nbuf};")
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
     w(f"    __shared__ int cnt_all[{G * 32}];  // count-only decode: per codeword, two iterations per word")
     w(f"    __shared__ uint32_t app_all[{G * S.N * S.WZ}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
@@ -1034,9 +1120,10 @@ def main():
         hb = np.loadtxt(os.path.join(res, fname), int, delimiter="\t")
         if G is None:
             G, P, Q = auto_geometry(hb, Z)
-        specs.append((Spec(tag, hb, Z, G, P, Q), not only or tag in only))
+        specs.append((Spec(tag, hb, Z, G, P, Q, pipe=PIPE), Spec(tag, hb, Z, G, P, Q), not only or tag in only))
     head = ["// GENERATED by gen_fused.py from the base graphs in resources/ -- do not edit.",
-            "#include <hip/hip_runtime.h>", '#include "nldpc_fused.h"', "namespace nldpc {"]
+            "#include <hip/hip_runtime.h>"]
+    head += ['#include "nldpc_fused.h"', "namespace nldpc {"]
     kinds = os.environ.get("NLDPC_GEN_KINDS")  # debug: instantiate a subset of kinds
     kinds = [int(k) for k in kinds.split(",")] if kinds else [0, 1, 2, 3]
 
@@ -1047,11 +1134,15 @@ def main():
             with open(path, "w") as f:
                 f.write(text)
 
-    for S, on in specs:
+    for S, SB_, on in specs:
         body = emit(S) if on else ""
+        # the SAVE kernels (training forward) keep the one-buffer schedule: with the pipelined one the
+        # cfg5 forward went from 22.0 to 31.4 ms (r2), while inference gained 6 %.  Each MODE is its own
+        # translation unit, so the two schedules never meet in one TU.
+        body_save = (emit(SB_) if on else "") if S.pipe else body
         for save in MODES:
             src = list(head)
-            src.append(body)
+            src.append(body_save if save == 1 else body)
             src.append(f"void* fused_{S.tag}_kernel_s{save}(int kind) {{")
             if on:
                 for k in kinds:
@@ -1061,7 +1152,7 @@ def main():
             src.append("}  // namespace nldpc")
             write(f"fused_{S.tag}_s{save}.hip", src)
         src = list(head)
-        src.append(emit_bwd(S) if on else "")
+        src.append(emit_bwd(SB_) if on else "")
         src.append(f"void* fused_{S.tag}_bwd(int kind) {{")
         if on:
             for k in kinds:
@@ -1071,7 +1162,7 @@ def main():
         src.append("}  // namespace nldpc")
         write(f"fused_{S.tag}_bwd.hip", src)
     src = list(head)
-    for S, _ in specs:
+    for S, _, _ in specs:
         for v in MODES:
             src.append(f"void* fused_{S.tag}_kernel_s{v}(int kind);")
         src.append(f"void* fused_{S.tag}_bwd(int kind);")
@@ -1079,7 +1170,7 @@ def main():
                    f"{{{', '.join(str(int(x)) for x in S.hb.reshape(-1))}}};")
     src.append("const FusedSpec* fused_specs(int* n) {")
     src.append(f"    static const FusedSpec tab[{len(specs)}] = {{")
-    for S, _ in specs:
+    for S, _, _ in specs:
         ks = ", ".join("{" + ", ".join(f"fused_{S.tag}_kernel_s{v}({k})" for k in range(4)) + "}" for v in MODES)
         kb = ", ".join(f"fused_{S.tag}_bwd({k})" for k in range(4))
         src.append(f"        {{\"{S.tag}\", {S.M}, {S.N}, {S.Z}, {S.E}, {S.G}, {S.threads}, basegraph_{S.tag}, "

@@ -121,7 +121,22 @@ static hipError_t add_launch(float* y, const float* x, int64_t n, hipStream_t s)
     return hipGetLastError();
 }
 
-// out[r][c] += sum over b of part[r][b][c]  (r < rows, c < width), in ascending b
+// The weight gradients from their partials, in a fixed order (deterministic), two levels so that
+// thousands of partials per weight are summed by many workgroups:
+// level 1: part[r][k*CH][c] = sum over b in [k*CH, k*CH + CH) of part[r][b][c], ascending b (in place:
+//          each chunk's sum replaces its own first row, which only that thread reads)
+// level 2: out[r][c] += sum over k of part[r][k*CH][c], ascending k
+constexpr int kReduceChunk = 64;
+__global__ void reduce_chunks(float* __restrict__ part, int64_t nb, int64_t width) {
+    const int64_t r = blockIdx.y, k = blockIdx.x;
+    float* p = part + (r * nb + k * kReduceChunk) * width;
+    const int64_t nrow = nb - k * kReduceChunk < kReduceChunk ? nb - k * kReduceChunk : kReduceChunk;
+    for (int64_t c = threadIdx.x; c < width; c += blockDim.x) {
+        float s = 0.f;
+        for (int64_t b = 0; b < nrow; ++b) s += p[b * width + c];
+        p[c] = s;
+    }
+}
 __global__ void reduce_partials(const float* __restrict__ part, int64_t rows, int64_t nb, int64_t width,
                                 float* __restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -129,7 +144,7 @@ __global__ void reduce_partials(const float* __restrict__ part, int64_t rows, in
     const int64_t r = t / width, c = t - r * width;
     const float* p = part + r * nb * width + c;
     float s = 0.f;
-    for (int64_t b = 0; b < nb; ++b) s += p[b * width];
+    for (int64_t b = 0; b < nb; b += kReduceChunk) s += p[b * width];
     out[t] += s;
 }
 
@@ -355,9 +370,11 @@ static WorkLayout work_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
     return w;
 }
 
-static hipError_t reduce_launch(const float* part, int64_t rows, int64_t nb, int64_t width, float* out, hipStream_t s) {
+static hipError_t reduce_launch(float* part, int64_t rows, int64_t nb, int64_t width, float* out, hipStream_t s) {
     const int64_t n = rows * width;
     if (n == 0) return hipSuccess;
+    const int64_t nk = (nb + kReduceChunk - 1) / kReduceChunk;
+    hipLaunchKernelGGL(reduce_chunks, dim3((unsigned)nk, (unsigned)rows), dim3(256), 0, s, part, nb, width);
     hipLaunchKernelGGL(reduce_partials, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, rows, nb, width, out);
     return hipGetLastError();
 }

@@ -11,7 +11,6 @@ mkdir -p $OUT/obj $OUT/gen
 for f in nldpc_graph.cpp nldpc_profile.cpp nldpc_forward.hip nldpc_backward.hip nldpc_aux.hip; do
     cp -p $P/lib/obj/$f.o $OUT/obj/
 done
-cp -p $P/lib/nldpc_tanh_ref.bin $OUT/ 2>/dev/null || true
 cd $P/csrc
 env "$@" NLDPC_GEN_ONLY=bg2_z384 NLDPC_GEN_KINDS=3 python3 gen_fused.py $OUT/gen $R/resources
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function -fno-slp-vectorize -I$R/include -I$P/csrc"

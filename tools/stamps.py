@@ -38,3 +38,8 @@ for n in names:
 # per-part VN time (waves 2p, 2p+1 form part p when parts are 2 waves)
 vn = np.stack([st[:, :, it, 1] - st[:, :, it - 1, 7].max(axis=1)[:, None] for it in range(1, T)]).mean(axis=(0, 1))
 print("VN cycles per wave:", " ".join(f"{v:.0f}" for v in vn))
+# every phase per wave (arrival minus the release the phase started from)
+for k, n in zip(range(2, 8), names[1:]):
+    per = np.stack([st[:, :, it, k] - st[:, :, it, k - 1].max(axis=1)[:, None] if k > 2 else
+                    st[:, :, it, k] - st[:, :, it, k - 1] for it in range(1, T)]).mean(axis=(0, 1))
+    print(f"{n + ' per wave:':20s}", " ".join(f"{v:.0f}" for v in per))
