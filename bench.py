@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel timing")
     ap.add_argument("--no-sweep", action="store_true", help="skip the Eb/N0 1..4 dB BER sweep")
     ap.add_argument("--no-count-only", action="store_true", help="skip the count-only decode timing (F2)")
+    ap.add_argument("--nw", default="1,1,2", help="cfg3ucn: NodeWeightSharingConfig (cn, ucn, vn) codes")
+    ap.add_argument("--kind", default="MS", choices=("MS", "QMS", "SP"), help="cfg3ucn: Boosted decoding type")
     return ap.parse_args()
 
 
@@ -286,8 +288,9 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
         from boosted_neural_ldpc_decoder.struct.NodeWeightSharingConfig import NodeWeightSharingConfig
         from nldpc.channel import boosted_code_rate
         conn = ConnectingMatrixTorch(ConnectingMatrix(Z, bg), device=dev)
-        model = BoostedNeuralLDPCDecoder(T, B, conn, node_weight_sharing_config=NodeWeightSharingConfig(1, 1, 2),
-                                         decoding_type=DecoderType.MS).to(dev)
+        nw = tuple(int(v) for v in args.nw.split(","))
+        model = BoostedNeuralLDPCDecoder(T, B, conn, node_weight_sharing_config=NodeWeightSharingConfig(*nw),
+                                         decoding_type=getattr(DecoderType, args.kind)).to(dev)
         model.eval()
         rate = boosted_code_rate(N, M)
     else:
@@ -350,8 +353,8 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
     bits_total = world * B * N * Z
     tag = {"cfg3": "bg2_z384", "cfg3ucn": "bg2_z384", "cfg2": "wimax_z24"}.get(args.workload, f"z{Z}")
     wl = {"cfg3": f"cfg3 Neural BG2 set0 z={Z}, T={T}, all T posteriors written",
-          "cfg3ucn": f"cfg3 decode with BoostedNeuralLDPCDecoder MS NW(1,1,2) (UCN on), BG2 set0 z={Z}, T={T}, "
-                     "all T posteriors written",
+          "cfg3ucn": f"cfg3 decode with BoostedNeuralLDPCDecoder {args.kind} NW({args.nw}) "
+                     f"(UCN {'on' if args.nw.split(',')[1] != '0' else 'off'}), BG2 set0 z={Z}, T={T}, all T posteriors written",
           "cfg2": f"cfg2 Neural WiMAX N=576 R=3/4 z={Z}, T={T}, all T posteriors written"}[args.workload]
     res = {
         "metric": METRIC,

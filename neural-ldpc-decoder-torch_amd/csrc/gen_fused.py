@@ -41,6 +41,7 @@ CN_PAIR_MAXDC = int(os.environ.get("NLDPC_GEN_CNPAIR", "0"))
 # build): a v_pk_add_f32 occupies the SIMD for 8 cycles against 2 for v_add_f32, so packing costs
 # time per element; scalar is the default
 PACK_VN = os.environ.get("NLDPC_GEN_PACK") == "1"
+PACK_MAX = int(os.environ.get("NLDPC_GEN_PACKMAX", "0"))
 # experiment knob: no opaque row base in the check-node phase (lets the compiler prove the row copies'
 # LDS slots disjoint and overlap them, at its own register cost)
 NORO = os.environ.get("NLDPC_GEN_NORO") == "1"
@@ -200,43 +201,48 @@ def emit(S: Spec) -> str:
     # additions run as packed fp32 (v_pk_add_f32: two IEEE adds per lane, same rounding); an odd
     # copy count leaves one scalar array.  The channel values a thread needs every iteration are
     # loaded once into registers (xp*/xs for its register columns, xd for its degree-1 columns).
-    NPAIR = Q // 2 if PACK_VN else 0
-    NSINGLE = Q - 2 * NPAIR
+    # per part: PACK_VN packs every part; PACK_MAX packs the parts whose register state (slots x Q)
+    # stays within that many registers (the heavy parts stay scalar, clear of the 128-VGPR cap)
+    def NP(p):
+        return Q // 2 if (PACK_VN or len(S.slots[p]) * Q <= PACK_MAX) else 0
 
-    def ref(q, k):
-        if q < 2 * NPAIR:
+    def NS(p):
+        return Q - 2 * NP(p)
+
+    def ref(p, q, k):
+        if q < 2 * NP(p):
             return f"cp{q // 2}[{k}].{'x' if q % 2 == 0 else 'y'}"
-        return f"cs{q - 2 * NPAIR}[{k}]"
+        return f"cs{q - 2 * NP(p)}[{k}]"
 
     def xref(p, j, q):
         cols = S.reg_cols[p]
         if j in cols:
             n = cols.index(j)
-            return f"xp{q // 2}[{n}].{'x' if q % 2 == 0 else 'y'}" if q < 2 * NPAIR else f"xs{q - 2 * NPAIR}[{n}]"
+            return f"xp{q // 2}[{n}].{'x' if q % 2 == 0 else 'y'}" if q < 2 * NP(p) else f"xs{q - 2 * NP(p)}[{n}]"
         n = S.d1_cols[p].index(j)
         return f"xd[{n * Q + q}]"
 
     def state_params(p, const=False):
         sp = len(S.slots[p])
         c = "const " if const else ""
-        ps = [f"{c}f2 (&cp{i})[{max(sp, 1)}]" for i in range(NPAIR)]
-        for i in range(NSINGLE):
+        ps = [f"{c}f2 (&cp{i})[{max(sp, 1)}]" for i in range(NP(p))]
+        for i in range(NS(p)):
             ps.append(f"{c}float (&cs{i})[{max(sp, 1)}]")
         return ", ".join(ps)
 
-    def state_args():
-        return ", ".join([f"cp{i}" for i in range(NPAIR)] + [f"cs{i}" for i in range(NSINGLE)])
+    def state_args(p):
+        return ", ".join([f"cp{i}" for i in range(NP(p))] + [f"cs{i}" for i in range(NS(p))])
 
     def x_params(p):
         nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
-        ps = [f"const f2 (&xp{i})[{nr}]" for i in range(NPAIR)]
-        for i in range(NSINGLE):
+        ps = [f"const f2 (&xp{i})[{nr}]" for i in range(NP(p))]
+        for i in range(NS(p)):
             ps.append(f"const float (&xs{i})[{nr}]")
         ps.append(f"const float (&xd)[{nd}]")
         return ", ".join(ps)
 
-    def x_args():
-        return ", ".join([f"xp{i}" for i in range(NPAIR)] + [f"xs{i}" for i in range(NSINGLE)] + ["xd"])
+    def x_args(p):
+        return ", ".join([f"xp{i}" for i in range(NP(p))] + [f"xs{i}" for i in range(NS(p))] + ["xd"])
 
     # ---------------------------------------------------------------- variable nodes
     # global accesses: bload/bstore(descriptor, lane byte offset vo, constant byte offset)
@@ -249,8 +255,8 @@ def emit(S: Spec) -> str:
         (last copy) are emitted interleaved, so consecutive adds never depend on each other (gfx950
         puts an s_nop between two dependent packed adds).  Each chain is the reference's sequential
         fp32 order: S_k = ((P_{k-1} + c_{k+1}) + ...) + c_{d-1}, v2c_k = x0 + S_k, P_k = P_{k-1} + c_k."""
-        grp = [("f2", f"cp{i}", f"xp{i}[{n}]", str(i)) for i in range(NPAIR)]
-        for i in range(NSINGLE):
+        grp = [("f2", f"cp{i}", f"xp{i}[{n}]", str(i)) for i in range(NP(p))]
+        for i in range(NS(p)):
             grp.append(("float", f"cs{i}", f"xs{i}[{n}]", f"s{i}"))
 
         def add(T_, x, y):
@@ -321,7 +327,7 @@ def emit(S: Spec) -> str:
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
                 vn_col(p, n, j, s, d, final)
-                for i in range(NPAIR):
+                for i in range(NP(p)):
                     w("            {")
                     w(f"            const f2 xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? f2{{bload(xr, vo, {X(j, 2 * i)}), "
                       f"bload(xr, vo, {X(j, 2 * i + 1)})}} : xp{i}[{n}];")
@@ -337,8 +343,8 @@ def emit(S: Spec) -> str:
                     w(f"                put_post<CM>(pr, vo, {X(j, 2 * i + 1)}, y_.y, ps);")
                     w("            }")
                     w("            }")
-                for i in range(NSINGLE):
-                    q = 2 * NPAIR + i
+                for i in range(NS(p)):
+                    q = 2 * NP(p) + i
                     w("            {")
                     w(f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : xs{i}[{n}];")
                     w("            float y_;")
@@ -390,8 +396,8 @@ def emit(S: Spec) -> str:
             w("    asm volatile(\"\" : \"+v\"(u));  // LDS addresses are recomputed here, not hoisted out of the loop")
             for q in range(Q):
                 for k, e in mine:
-                    w(f"    lds[{own(e, q, e0)}] = {ref(q, k)};")
-                    w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(q, k)}, a.qbit);")
+                    w(f"    lds[{own(e, q, e0)}] = {ref(p, q, k)};")
+                    w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(p, q, k)}, a.qbit);")
             if d1:  # v2c = (0 + xin) + 0: no other edge in the column (bypass: the check node reads xa)
                 w("    if constexpr (!D1_BYPASS) {")
             for j, e in d1:
@@ -408,7 +414,7 @@ def emit(S: Spec) -> str:
             w("    asm volatile(\"\" : \"+v\"(u));")
             for q in range(Q):
                 for k, e in mine:
-                    w(f"    {ref(q, k)} = lds[{own(e, q, e0)}];")
+                    w(f"    {ref(p, q, k)} = lds[{own(e, q, e0)}];")
             if d1:  # this iteration's posterior right away (bypass: written by the check node)
                 w("    if constexpr (!D1_BYPASS) {")
             for j, e in d1:
@@ -572,24 +578,24 @@ def emit(S: Spec) -> str:
         w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw) {{")
-        for i in range(NPAIR):
+        for i in range(NP(p)):
             w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
-        for i in range(NSINGLE):
+        for i in range(NS(p)):
             w(f"    float cs{i}[{sp}], xs{i}[{nr}];")
         w(f"    float xd[{nd}];")
         w("#pragma unroll")
         w(f"    for (int k = 0; k < {sp}; ++k) {{")
-        for i in range(NPAIR):
+        for i in range(NP(p)):
             w(f"        cp{i}[k] = f2{{0.f, 0.f}};")
-        for i in range(NSINGLE):
+        for i in range(NS(p)):
             w(f"        cs{i}[k] = 0.f;")
         w("    }")
         w("    // this thread's channel values, loaded once for all T iterations")
         for n, j in enumerate(S.reg_cols[p]):
-            for i in range(NPAIR):
+            for i in range(NP(p)):
                 w(f"    xp{i}[{n}] = f2{{bload(xr, vo, {X(j, 2 * i)}), bload(xr, vo, {X(j, 2 * i + 1)})}};")
-            for i in range(NSINGLE):
-                w(f"    xs{i}[{n}] = bload(xr, vo, {X(j, 2 * NPAIR + i)});")
+            for i in range(NS(p)):
+                w(f"    xs{i}[{n}] = bload(xr, vo, {X(j, 2 * NP(p) + i)});")
         for n, j in enumerate(S.d1_cols[p]):
             for q in range(Q):
                 w(f"    xd[{n * Q + q}] = bload(xr, vo, {X(j, q)});")
@@ -609,10 +615,10 @@ def emit(S: Spec) -> str:
         def chan_steps(step_expr, indent):
             w(f"{indent}{{ const cfloat_p wr_ = (cfloat_p)(a.w_vn + (int64_t)({step_expr}) * N);")
             for n, j in enumerate(S.reg_cols[p]):
-                for i in range(NPAIR):
+                for i in range(NP(p)):
                     for c in "xy":
                         w(f"{indent}  xp{i}[{n}].{c} = chan_step<KIND>(xp{i}[{n}].{c}, a, wr_[{j}]);")
-                for i in range(NSINGLE):
+                for i in range(NS(p)):
                     w(f"{indent}  xs{i}[{n}] = chan_step<KIND>(xs{i}[{n}], a, wr_[{j}]);")
             for n, j in enumerate(S.d1_cols[p]):
                 for q in range(Q):
@@ -659,7 +665,7 @@ def emit(S: Spec) -> str:
         w("        const uint8_t* pmp = (SAVE && a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t pm = make_rsrc((const float*)(pmp ? pmp + blk * {NZ} : nullptr), pmp ? nlive * {NZ} : 0);")
         if "vn" not in SKIP:
-            w(f"        vn_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
+            w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
         w(f"        if constexpr (CNT) {{ if (it >= 1) ps.{cnt_flush}({cnt_slot}, it - 1); else ps.ec = 0; }}")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
@@ -701,14 +707,14 @@ def emit(S: Spec) -> str:
 
         def op_w(ci):
             preload(ci)
-            w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, {buf(ci)}, u, a, it, sv, vc);")
+            w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, it, sv, vc);")
 
         def op_cn(ci):
             if "cn" not in SKIP:
                 w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw);")
 
         def op_r(ci):
-            w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args()}, {x_args()}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
+            w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
               f"ps, d1m);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
                 w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
@@ -756,12 +762,12 @@ def emit(S: Spec) -> str:
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
         w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
-        w(f"    post_p{p}<KIND, MODE>({state_args()}, {x_args()}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr);")
+        w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr);")
         w(f"    if constexpr (CNT) ps.{cnt_flush}({cnt_slot}, a.T - 1);")
         w("    if (a.c2v_out) {")
         for q in range(Q):
             for k, e in enumerate(S.slots[p]):
-                w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, {ref(q, k)});")
+                w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, {ref(p, q, k)});")
         w("    }")
         w("}")
     w("template <int KIND, int MODE>")

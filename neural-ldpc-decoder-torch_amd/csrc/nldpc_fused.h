@@ -169,6 +169,81 @@ __device__ __forceinline__ void two_smallest(const uint32_t (&key)[DC], uint32_t
     }
 }
 
+// The two smallest of |m_k| (as a multiset) in the float domain, |m_k| as a source modifier.  Inline
+// asm: written as fminf/fmaxf the compiler materialises every fabsf (v_and_b32) and, in IEEE mode,
+// canonicalises each operand (v_max_f32 x, x) -- three extra VALU per edge.  Plain VALU, no hazards.
+__device__ __forceinline__ float min_aa(float x, float y) {
+    float d;
+    asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(d) : "v"(x), "v"(y));
+    return d;
+}
+__device__ __forceinline__ float max_aa(float x, float y) {
+    float d;
+    asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(d) : "v"(x), "v"(y));
+    return d;
+}
+__device__ __forceinline__ float min_a(float a, float x) {  // min(a, |x|), a >= 0
+    float d;
+    asm("v_min_f32_e64 %0, %1, |%2|" : "=v"(d) : "v"(a), "v"(x));
+    return d;
+}
+__device__ __forceinline__ float med3_a(float a, float b, float x) {  // med3(a, b, |x|)
+    float d;
+    asm("v_med3_f32 %0, %1, %2, |%3|" : "=v"(d) : "v"(a), "v"(b), "v"(x));
+    return d;
+}
+
+template <int DC>
+__device__ __forceinline__ void two_smallest_abs(const float (&m)[DC], float& min1, float& min2) {
+    if constexpr (DC == 1) {
+        min1 = fabsf(m[0]);
+        min2 = __builtin_inff();
+    } else {
+        float a = min_aa(m[0], m[1]), b = max_aa(m[0], m[1]);
+#pragma unroll
+        for (int k = 2; k < DC; ++k) {
+            b = med3_a(a, b, m[k]);
+            a = min_a(a, m[k]);
+        }
+        min1 = a;
+        min2 = b;
+    }
+}
+
+#ifndef NLDPC_CN_KEYS
+// Float-domain form (default): per edge two min-tracking ops, the argmin compare with |m_k| as a
+// modifier, the epilogue and the sign -- no per-edge key and no per-row key decode.  Exact zeros
+// (the reference's "masked" entries: 0 counts as 10000 in the minimum, and is not positive) are rare
+// after iteration 0; a row copy in which any lane of the wave sees one (min1 == 0) takes a
+// wave-uniform branch that maps each 0 to -20000 (magnitude above the 10000 clamp, not positive) and
+// tracks the minimum again.  Bit-identical to the key form below (-DNLDPC_CN_KEYS) and to cn_core.
+template <int DC>
+__device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
+    float min1, min2;
+    two_smallest_abs<DC>(m, min1, min2);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(min1 == 0.f) != 0, 0)) {
+#pragma unroll
+        for (int k = 0; k < DC; ++k) m[k] = m[k] == 0.f ? -20000.f : m[k];
+        two_smallest_abs<DC>(m, min1, min2);
+    }
+    bool pos[DC];
+    bool par = false;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        pos[k] = m[k] > 0.f;
+        par ^= pos[k];
+    }
+    float mg1 = __builtin_amdgcn_fmed3f(min1, 0.f, 10000.f);  // the masked tile entries (10000) take part
+    float mg2 = __builtin_amdgcn_fmed3f(min2, 0.f, 10000.f);  // in the min (min1, min2 >= 0: a clamp)
+    asm volatile("" : "+v"(mg1), "+v"(mg2));
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
+        const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
+        m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
+    }
+}
+#else
 template <int DC>
 __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
     constexpr uint32_t kInit = (0x461C4000u << 1) - 2u;  // key of 10000.f
@@ -195,6 +270,7 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
     }
 }
+#endif
 
 // Backward of the fused decoder (training): one workgroup per G codewords walks the iterations in
 // reverse with dL/dc2v in registers (same ownership as the forward's c2v), reading only the saved
