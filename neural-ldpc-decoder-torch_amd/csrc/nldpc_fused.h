@@ -386,8 +386,8 @@ __device__ __forceinline__ void PostSink::flush_wave(int* cntl, int it) {
 // as one sign select.  Results equal cn_core + cn_epilogue (a zero c2v may differ in its sign bit
 // only, which no sum of the decoder can observe).  ~19 VALU per edge copy instead of ~45.
 template <int DC, int KIND>
-__device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC], bool has_w, int qbit, float lo,
-                                            float hi, bool ucn, float uf, const float (&wu)[DC]) {
+__device__ __forceinline__ void boosted_row_keys(float (&m)[DC], const float (&w)[DC], bool has_w, int qbit, float lo,
+                                                 float hi, bool ucn, float uf, const float (&wu)[DC]) {
     constexpr uint32_t kInit = 0x461C4000u << 1;  // key of 10000.f
     uint32_t key[DC];
     bool pos[DC];
@@ -431,6 +431,73 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
         const bool neg = KIND == NLDPC_MS && (sel ? n2 : n1);
         m[k] = ((par != pos[k]) != neg) ? x3 : -x3;
     }
+}
+
+// Float-domain form of boosted_row (r2), the two smallest of |m| tracked with |m| as a source modifier
+// as in neural_row (2 VALU per edge), no per-edge conditioning, zero fix or key.  What makes the raw
+// magnitudes enough: each edge's c2v magnitude is "min over the OTHER edges" of the conditioned values,
+// and min over others commutes with any non-decreasing map of |m|:
+//  * MS with a symmetric clip (lo == -hi): |clamp(m)| = min(|m|, hi).  The zero fix (0 -> 1e-4) is not
+//    monotone, and a minimum <= 1e-4 changes sign in the magnitude correction, so a row copy in which
+//    any lane of the wave has min1 <= 1e-4 (exact zeros: punctured columns in the first iteration) takes
+//    the key form above (wave-uniform branch).
+//  * active QMS: Q is odd and non-decreasing, |Q(m)| = Q(|m|); the zero fix maps Q's 0 to 1e-4 and the
+//    magnitude correction maps 1e-4 back to 0 (every nonzero Q value is >= the 0.5 grid step), so the
+//    magnitude is Q(min over others |m|) in every case.  pos_k = Q(m_k) >= 0 (zeros are fixed to +1e-4)
+//    = m_k >= -0.5 / s (the scaling by s is exact).
+// The epilogue clip/Q(relu(.)) is one med3 (relu folds into the lower bound); UCN flags are 0/1, so
+// the reference's (|x| w)(1 - u) + (|x| w_u) u is exactly |x| w or |x| w_u (a select).  DC == 1 rows
+// (the masked 10000 would be the magnitude) keep the key form.  Equal to boosted_row_keys up to the
+// sign bit of a zero c2v, which no sum of the decoder observes.
+template <int DC, int KIND>
+__device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC], bool has_w, int qbit, float lo,
+                                            float hi, bool ucn, float uf, const float (&wu)[DC]) {
+    if constexpr (DC >= 2) {
+        float min1, min2;
+        two_smallest_abs<DC>(m, min1, min2);
+        bool fast = true;
+        if constexpr (KIND == NLDPC_MS)
+            fast = lo == -hi && hi > kZeroFix && __builtin_amdgcn_ballot_w64(min1 <= kZeroFix) == 0;
+        if (__builtin_expect(fast, 1)) {
+            float mg1, mg2, thr, top, inv;
+            if constexpr (KIND == NLDPC_MS) {
+                mg1 = fminf(min1, hi);
+                mg2 = fminf(min2, hi);
+                thr = 0.f;
+                top = hi;
+                inv = 1.f;
+            } else {
+                const float s = qbit == 5 ? 2.f : (qbit == 3 ? 0.5f : 1.f);
+                inv = qbit == 5 ? 0.5f : (qbit == 3 ? 2.f : 1.f);
+                top = qbit == 6 ? 15.5f : (qbit == 5 ? 15.f : (qbit == -5 ? 15.f : (qbit == 4 ? 7.f : 3.f)));  // hi * s
+                // s * Q(min) = min(rint(min s), hi s): the magnitude pre-scaled by s, so the per-edge
+                // product (s mag) w = s (mag w) exactly and Q's own scaling needs no multiply
+                mg1 = fminf(rintf(fmul(min1, s)), top);
+                mg2 = fminf(rintf(fmul(min2, s)), top);
+                thr = fmul(-0.5f, inv);
+            }
+            asm volatile("" : "+v"(mg1), "+v"(mg2));
+            const float lo0 = KIND == NLDPC_MS ? fmaxf(lo, 0.f) : 0.f;
+            bool pos[DC];
+            bool par = false;
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {
+                pos[k] = KIND == NLDPC_MS ? m[k] > 0.f : m[k] >= thr;
+                par ^= pos[k];
+            }
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {
+                const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
+                const float x1 = !has_w ? mag : fmul(mag, (ucn && uf != 0.f) ? wu[k] : w[k]);
+                float x3;
+                if constexpr (KIND == NLDPC_MS) x3 = __builtin_amdgcn_fmed3f(x1, lo0, top);
+                else x3 = fmul(__builtin_amdgcn_fmed3f(rintf(x1), 0.f, top), inv);
+                m[k] = (par != pos[k]) ? x3 : -x3;
+            }
+            return;
+        }
+    }
+    boosted_row_keys<DC, KIND>(m, w, has_w, qbit, lo, hi, ucn, uf, wu);
 }
 
 // check node of one check copy in place (m: gathered v2c -> c2v), every kind: Neural through the
