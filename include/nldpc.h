@@ -83,10 +83,11 @@ int nldpc_graph_dims(const nldpc_graph* g, int32_t* dims);
 int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t* shift);
 
 /* ---- execution path.  *eligible = 1 when nldpc_forward with these arguments runs the fused
- *      register-resident kernel (a base graph / lifting size compiled in, no UCN, fresh state,
- *      T <= 64; saving for backward included, except QMS with an identity quantiser): then v2c is
- *      unused, and c2v is unused too with NLDPC_FLAG_NO_STATE.  Otherwise the streaming kernels run
- *      and need both buffers. */
+ *      register-resident kernel: a (base graph, lifting size) compiled in, no incoming message state
+ *      (c2v_in == 0; a resumed UCN segment passes app_prev instead), T <= 64, no NLDPC_FLAG_STREAM;
+ *      every kind, UCN and cumulative VN weights included, and saving for backward included except
+ *      QMS with an identity quantiser.  Then v2c is unused, and c2v is unused too with
+ *      NLDPC_FLAG_NO_STATE.  Otherwise the streaming kernels run and need both buffers. */
 int nldpc_fast_path(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, int32_t saving,
                     int32_t* eligible);
 

@@ -33,8 +33,9 @@ LDS_BYTES = 160 * 1024 - 2048  # leave room for the compiler / alignment
 
 
 def app_words(N, Z):
-    """32-bit words of one codeword's UCN hard-decision bit array (bit (j, v) = APP[j][v] >= 0)."""
-    return N * ((Z + 31) // 32)
+    """32-bit words of one codeword's UCN hard-decision bit array (bit (j, v) = APP[j][v] >= 0): per column
+    the Z bits and one more word (word 0 again, so a 32-bit window at any start reads two words)."""
+    return N * ((Z + 31) // 32 + 1)
 # check rows up to this degree let the compiler interleave their lane copies (more ILP, more registers)
 CN_PAIR_MAXDC = int(os.environ.get("NLDPC_GEN_CNPAIR", "0"))
 # VN lane copies as packed fp32 pairs (v_pk_add_f32) or all scalar chains.  Measured on gfx950 (stamp
@@ -73,6 +74,19 @@ for _item in filter(None, os.environ.get("NLDPC_FUSED_EXTRA", "").split(",")):
     _tag = f"{_g if _g in _GRAPH_FILES else os.path.splitext(os.path.basename(_g))[0]}_z{int(_z)}"
     if all(t[0] != _tag for t in SPECS):
         SPECS.append((_tag, _f, int(_z), None, None, None))
+
+# experiment knob: NLDPC_GEN_GEOM="bg2_z384:1,4,3" overrides a spec's (G, P, Q)
+for _item in filter(None, os.environ.get("NLDPC_GEN_GEOM", "").split(";")):
+    _t, _g = _item.split(":")
+    SPECS = [(t, f, z, *[int(v) for v in _g.split(",")]) if t == _t else (t, f, z, g, p, q) for t, f, z, g, p, q in SPECS]
+
+# Boosted with cumulative VN weights: the posterior re-reads xa (the registers hold xin).  vmcnt counts
+# loads and stores together, in order, so a load issued after a posterior store waits for that store.
+# 2 (default) = every such load of a VN call (and of a read-back's degree-1 columns) issued before its
+# first store: cfg3 MS NW(1,0,2) 99.9 -> 92.5 ms, QMS NW(1,1,2) 234.7 -> 215.6 ms; 1 = at the start of
+# each column (slower: 124 -> 130 ms); 0 = next to each posterior
+XPRE = os.environ.get("NLDPC_GEN_XPRE", "2") == "1"
+XPRE2 = os.environ.get("NLDPC_GEN_XPRE", "2") == "2"
 
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
@@ -150,6 +164,14 @@ class Spec:
         self.smax = max(1, max(len(s) for s in self.slots)) * Q
         # row chunks: contiguous row ranges whose messages (edges x Z x G) fit in LDS beside the UCN bits
         self.WZ = (Z + 31) // 32
+        self.WZX = self.WZ + 1  # words per column in the bit array
+        # UCN by waves: every wave's 64 lanes are 64 consecutive copies of one codeword (ZT % 64 == 0) and
+        # the bit vectors are whole words (Z % 32 == 0).  The owners write the hard decisions by ballots
+        # (no LDS atomics, no clearing), and a check row's unsatisfied flags come from word windows of
+        # its columns' vectors XOR-ed once per row and wave, not gathered bit by bit per copy and edge.
+        # (used by the MS kernels only: in the QMS kernels the extra scalar state measured slower, 180 -> 217 ms
+        # at cfg3 NW(1,1,2), register allocation; UCNW in the generated code)
+        self.ucn_wave = self.ZT % 64 == 0 and Z % 32 == 0 and os.environ.get("NLDPC_GEN_UCNWAVE", "1") == "1"
         cap = ((LDS_BYTES - 4 * G * app_words(self.N, Z)) // (4 * G) - 32) // Z
         if pipe:  # two buffers; only the count-only counters (G*128 B) share the remaining KiB
             cap = ((160 * 1024 - 1024 - 4 * G * app_words(self.N, Z)) // (8 * G) - (32 if G > 1 else 0)) // Z
@@ -195,6 +217,7 @@ def emit(S: Spec) -> str:
     w("#define CNT (MODE >= 2)")
     w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
     w("#define D1_BYPASS (KIND == NLDPC_NEURAL && !SAVE)")
+    w(f"#define UCNW (KIND == NLDPC_MS && {'true' if S.ucn_wave else 'false'})  // UCN bits by waves (Spec.ucn_wave)")
     assert NZ < 65536  # per-codeword error counts are packed two to an LDS word
 
     # Register state of part p: copies are paired (q = 0,1 / 2,3 ...) into float2 arrays so the VN's
@@ -266,6 +289,12 @@ def emit(S: Spec) -> str:
             return "f2{0.f, 0.f}" if T_ == "f2" else "0.f"
 
         w(f"        {{  // column {j}, degree {d}")
+        if XPRE:  # the posterior's channel values (cumulative VN weights: xa from memory) issued first
+            for i in range(NP(p)):
+                w(f"            const f2 xl_{i} = (KIND != NLDPC_NEURAL && a.w_vn) ? f2{{bload(xr, vo, {X(j, 2 * i)}), "
+                  f"bload(xr, vo, {X(j, 2 * i + 1)})}} : xp{i}[{n}];")
+            for i in range(NS(p)):
+                w(f"            const float xl_s{i} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, 2 * NP(p) + i)}) : xs{i}[{n}];")
         for T_, arr, xin, g in grp:
             w(f"            {T_} P_{g} = {zero(T_)};")
         if not final:
@@ -323,14 +352,23 @@ def emit(S: Spec) -> str:
               f"uint32_t d1m, rsrc_t apr) {{")
             if not final:
                 w("    const bool ucn_ = KIND != NLDPC_NEURAL && a.ucn;  // UCN: hard decisions of the previous posterior")
+            if XPRE2 and NP(p) == 0:
+                # every posterior's xa (cumulative VN weights) requested before the first posterior store:
+                # a later load would wait (vmcnt counts in order) for every store issued before it
+                for n, j in enumerate(cols):
+                    for i in range(NS(p)):
+                        w(f"    const float xl_{n}_{i} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, i)}) : xs{i}[{n}];")
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
                 vn_col(p, n, j, s, d, final)
                 for i in range(NP(p)):
                     w("            {")
-                    w(f"            const f2 xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? f2{{bload(xr, vo, {X(j, 2 * i)}), "
-                      f"bload(xr, vo, {X(j, 2 * i + 1)})}} : xp{i}[{n}];")
+                    if XPRE:
+                        w(f"            const f2 xo_ = xl_{i};")
+                    else:
+                        w(f"            const f2 xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? f2{{bload(xr, vo, {X(j, 2 * i)}), "
+                          f"bload(xr, vo, {X(j, 2 * i + 1)})}} : xp{i}[{n}];")
                     w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w("                bool m0_, m1_;")
                     w(f"                bstore(pr, vo, {X(j, 2 * i)}, posterior_m<KIND>(xo_.x, P_{i}.x, a, m0_));")
@@ -346,7 +384,9 @@ def emit(S: Spec) -> str:
                 for i in range(NS(p)):
                     q = 2 * NP(p) + i
                     w("            {")
-                    w(f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : xs{i}[{n}];")
+                    w(f"            const float xo_ = xl_s{i};" if XPRE else
+                      f"            const float xo_ = xl_{n}_{i};" if (XPRE2 and NP(p) == 0) else
+                      f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : xs{i}[{n}];")
                     w("            float y_;")
                     w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w("                bool m_;")
@@ -359,7 +399,12 @@ def emit(S: Spec) -> str:
                     w("            }")
                     if not final:
                         app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xs{i}[{n}], a))"
-                        w(f"            if (ucn_) app_or(appw, {j * S.WZ}, u + {q * ZT}, (it == 0 ? {app0} : y_) >= 0.f);")
+                        b_ = f"(it == 0 ? {app0} : y_) >= 0.f"
+                        if S.ucn_wave:
+                            w(f"            if (ucn_) {{ if constexpr (UCNW) app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {b_}); "
+                              f"else app_or(appw, {j * S.WZX}, u + {q * ZT}, {b_}); }}")
+                        else:
+                            w(f"            if (ucn_) app_or(appw, {j * S.WZX}, u + {q * ZT}, {b_});")
                     w("            }")
                 w("        }")
                 w("        __builtin_amdgcn_sched_barrier(0);")
@@ -371,7 +416,12 @@ def emit(S: Spec) -> str:
                 for n, j in enumerate(S.d1_cols[p]):
                     for q in range(Q):
                         app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xd[{n * Q + q}], a))"
-                        w(f"        app_or(appw, {j * S.WZ}, u + {q * ZT}, it == 0 ? {app0} >= 0.f : ((d1m >> {n * Q + q}) & 1u) != 0u);")
+                        bit = f"it == 0 ? {app0} >= 0.f : ((d1m >> {n * Q + q}) & 1u) != 0u"
+                        if S.ucn_wave:
+                            w(f"        if constexpr (UCNW) app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {bit}); "
+                              f"else app_or(appw, {j * S.WZX}, u + {q * ZT}, {bit});")
+                        else:
+                            w(f"        app_or(appw, {j * S.WZX}, u + {q * ZT}, {bit});")
                 w("    }")
             w("}")
 
@@ -417,10 +467,17 @@ def emit(S: Spec) -> str:
                     w(f"    {ref(p, q, k)} = lds[{own(e, q, e0)}];")
             if d1:  # this iteration's posterior right away (bypass: written by the check node)
                 w("    if constexpr (!D1_BYPASS) {")
+            if XPRE2:
+                for j, e in d1:
+                    for q in range(Q):
+                        w(f"    const float xl_{j}_{q} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
             for j, e in d1:
                 for q in range(Q):
                     bit = S.d1_cols[p].index(j) * Q + q
-                    w(f"    {{ const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
+                    if XPRE2:
+                        w(f"    {{ const float xo_ = xl_{j}_{q};")
+                    else:
+                        w(f"    {{ const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
                     w(f"      const float P_ = fadd(0.f, lds[{own(e, q, e0)}]);")
                     w("      float y_;")
                     w("      if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
@@ -508,19 +565,42 @@ def emit(S: Spec) -> str:
                 i, q = rcs[n]
                 es = S.row_edges[i]
                 DC = len(es)
+                if S.ucn_wave and q == 0:
+                    # the row's unsatisfied flags for this wave's copies, all Q of them at once: lane 2q+h
+                    # XORs the 32-bit windows (copies u0 + q*ZT + 32h + 0..31, rotated by each edge's shift)
+                    # of the row's columns; the 2Q words become Q lane masks (bit l = lane l's flag)
+                    w(f"    uint64_t {', '.join(f'umr{i}_{qq} = 0' for qq in range(Q))};")
+                    w("    if (UCNW && a.ucn) {")
+                    w("        const int l_ = threadIdx.x & 63;")
+                    w(f"        const uint32_t bq_ = (uint32_t)(u - l_ + min(l_ >> 1, {Q - 1}) * {ZT} + (l_ & 1) * 32);")
+                    w(f"        uint32_t wl_[{DC}], wh_[{DC}], sh_[{DC}];  // all windows' words requested first")
+                    for k, e in enumerate(es):
+                        j = int(S.hb_cols[e])
+                        w(f"        app_win_load(appw + {j * S.WZX}, bq_ + {int(S.shift[e])}u, {Z}u, wl_[{k}], wh_[{k}], sh_[{k}]);")
+                    w("        uint32_t pw_ = 0u;")
+                    w(f"        for (int k = 0; k < {DC}; ++k) pw_ ^= __builtin_amdgcn_alignbit(wh_[k], wl_[k], sh_[k]);")
+                    for qq in range(Q):
+                        w(f"        umr{i}_{qq} = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(pw_, {2 * qq + 1}) << 32) | "
+                          f"(uint32_t)__builtin_amdgcn_readlane(pw_, {2 * qq});")
+                    w("    }")
                 w("    {")
                 w(f"        float wv[{DC}], bv[{DC}];")
                 w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{woff[i]} + k]; bv[k] = Bv[{woff[i]} + k]; }}")
                 w("        const bool wc = a.w_cn != nullptr;")
                 w("        float uf_ = 0.f;  // UCN: unsatisfied check (odd number of row variables with APP >= 0)")
                 w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
+                if S.ucn_wave:
+                    w(f"            if constexpr (UCNW) uf_ = __builtin_amdgcn_inverse_ballot_w64(umr{i}_{q}) ? 1.f : 0.f;")
+                    w("            else {")
                 w("            uint32_t par_ = 0;")
                 for k, e in enumerate(es):
                     c, _ = rot(e, q)
                     j = int(S.hb_cols[e])
                     vexpr = f"u + {c}" if c + ZT <= Z else f"u + {c} - (u >= {Z - c} ? {Z} : 0)"
-                    w(f"            {{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZ} + (v_ >> 5)] >> (v_ & 31); }}")
+                    w(f"            {{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZX} + (v_ >> 5)] >> (v_ & 31); }}")
                 w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
+                if S.ucn_wave:
+                    w("            }")
                 w("        }")
                 if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
                     w(f"        cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
@@ -642,7 +722,7 @@ def emit(S: Spec) -> str:
         w("    uint32_t d1m = 0;  // UCN: hard decisions of this thread's degree-1 posteriors")
         w(f"    const rsrc_t apr = make_rsrc(a.app_prev ? a.app_prev + blk * {NZ} : a.xa, a.app_prev ? nlive * {4 * NZ} : 0);")
         w("    if (KIND != NLDPC_NEURAL && a.ucn) {")
-        w(f"        for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZ}; i_ += {S.threads}) app_all[i_] = 0u;")
+        w(f"        for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
         w("        __syncthreads();")
         w("    }")
         w("    for (int it = 0; it < a.T; ++it) {")
@@ -717,8 +797,8 @@ def emit(S: Spec) -> str:
             w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
               f"ps, d1m);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
-                w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
-                w(f"            for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZ}; i_ += {S.threads}) app_all[i_] = 0u;")
+                w("        if (KIND != NLDPC_NEURAL && !UCNW && a.ucn) {")
+                w(f"            for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
                 w("        }")
 
         K = len(S.chunks)
@@ -755,8 +835,8 @@ def emit(S: Spec) -> str:
             # R_{K-1} (buffer 0) in other waves -> keep a barrier; K even: R_{K-1} reads buffer 1
             if K % 2 == 1:
                 w("        __syncthreads();")
-            else:  # UCN: the hard-decision bits cleared in R_{K-1} must be clear before any wave's next VN
-                w("        if (KIND != NLDPC_NEURAL && a.ucn) __syncthreads();")
+            else:  # UCN: the bits cleared in R_{K-1} must be clear before any wave's next VN
+                w("        if (KIND != NLDPC_NEURAL && !UCNW && a.ucn) __syncthreads();")
         w("    }")
         w("    const float* pl = a.outs.p[a.T - 1];")
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
@@ -790,8 +870,8 @@ def emit(S: Spec) -> str:
     w(f"    float* lds = lds_all + g * {CF * S.nbuf};")
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
     w(f"    __shared__ int cnt_all[{G * 32}];  // count-only decode: per codeword, two iterations per word")
-    w(f"    __shared__ uint32_t app_all[{G * S.N * S.WZ}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
-    w(f"    uint32_t* appw = app_all + g * {S.N * S.WZ};")
+    w(f"    __shared__ uint32_t app_all[{G * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
+    w(f"    uint32_t* appw = app_all + g * {S.N * S.WZX};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
     each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all, app_all, appw)", indent="    ")
     w("    if constexpr (CNT) {")
@@ -800,6 +880,7 @@ def emit(S: Spec) -> str:
     w("    }")
     w("}")
     w("#undef D1_BYPASS")
+    w("#undef UCNW")
     w("#undef SAVE")
     w("#undef CNT")
     w("#undef CM")

@@ -70,23 +70,29 @@ constexpr int saved_msg_bytes() { return KIND == NLDPC_QMS ? 1 : 4; }
 // Channel value the VN adds.  With cumulative VN weights (Boosted, w_vn set) the registers hold xin
 // itself, advanced one step per iteration by chan_step (Boosted…py:325-337: xin <- Q(xin * w_t)),
 // so the chain is never re-run from xa; otherwise they hold xa and QMS quantises it (idempotent).
+// QMS quantiser of the channel values and posteriors in the fused kernels
+// (the generic quantize(): the four-operation quantize_active behind a select measured 15 % slower in the
+// fused QMS kernels, cfg3 NW(1,1,2) 187.6 -> 217 ms -- register allocation, not operation count)
+__device__ __forceinline__ float qms_q(float x, int q) { return quantize(x, q); }
+
 template <int KIND>
 __device__ __forceinline__ float chan(float x, const FusedArgs& a) {
     if (KIND == NLDPC_NEURAL || a.w_vn) return x;
-    return KIND == NLDPC_QMS ? quantize(x, a.qbit) : x;
+    return KIND == NLDPC_QMS ? qms_q(x, a.qbit) : x;
 }
 template <int KIND>
 __device__ __forceinline__ float chan_step(float x, const FusedArgs& a, float w) {
     x = fmul(x, w);
-    return KIND == NLDPC_QMS ? quantize(x, a.qbit) : x;
+    return KIND == NLDPC_QMS ? qms_q(x, a.qbit) : x;
 }
 
-// posterior of one variable copy: Neural xa + P; Boosted clamp(Q(xa) + P) (Boosted…py:513-521)
+// posterior of one variable copy: Neural xa + P; Boosted clamp(Q(xa) + P) (Boosted…py:513-521), the
+// clamp as one med3 (the same value for every non-NaN sum; lo <= hi)
 template <int KIND>
 __device__ __forceinline__ float posterior(float xav, float P, const FusedArgs& a) {
     if (KIND == NLDPC_NEURAL) return fadd(xav, P);
-    const float xo = (KIND == NLDPC_QMS) ? quantize(xav, a.qbit) : xav;
-    return clampf(fadd(xo, P), a.lo, a.hi);
+    const float xo = (KIND == NLDPC_QMS) ? qms_q(xav, a.qbit) : xav;
+    return __builtin_amdgcn_fmed3f(fadd(xo, P), a.lo, a.hi);
 }
 
 // Two variable copies at once.  f2 arithmetic is per-lane IEEE fp32 (v_pk_add_f32 on gfx950: two
@@ -109,7 +115,7 @@ __device__ __forceinline__ void save_v2c(rsrc_t r, uint32_t vc, int elem, float 
 // Boosted posterior and its clamp mask (saved for the backward): in_range of the pre-clamp value
 template <int KIND>
 __device__ __forceinline__ float posterior_m(float xav, float P, const FusedArgs& a, bool& m) {
-    const float xo = (KIND == NLDPC_QMS) ? quantize(xav, a.qbit) : xav;
+    const float xo = (KIND == NLDPC_QMS) ? qms_q(xav, a.qbit) : xav;
     const float yp = fadd(xo, P);
     m = yp >= a.lo && yp <= a.hi;
     return clampf(yp, a.lo, a.hi);
@@ -126,6 +132,30 @@ __device__ __forceinline__ f2 chan2(f2 x, const FusedArgs& a) {
 // the bits of its row's variables at (h + s_e) mod Z and takes their parity (odd = unsatisfied).
 __device__ __forceinline__ void app_or(uint32_t* appw, int base, int v, bool bit) {
     if (bit) atomicOr(appw + base + (v >> 5), 1u << (v & 31));
+}
+
+// The same bits written a wave at a time (geometries whose waves hold 64 consecutive copies u0 + l of
+// one codeword, Z % 32 == 0): one ballot, two words by lane 0, word 0 repeated at word WZ so that a
+// 32-bit window starting anywhere in [0, Z) lies in two consecutive words.  Every word is rewritten each
+// iteration: no atomics and no clearing.
+template <int WZ>
+__device__ __forceinline__ void app_wave(uint32_t* col, int u, bool bit) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(bit);
+    if ((threadIdx.x & 63) == 0) {
+        const int wi = u >> 5;
+        col[wi] = (uint32_t)m;
+        col[wi + 1] = (uint32_t)(m >> 32);
+        if (wi == 0) col[WZ] = (uint32_t)m;
+    }
+}
+// the two words holding bits b .. b+31 (cyclic mod Z) of a column's vector, b in [0, 2Z), and the shift:
+// the window is alignbit(hi, lo, sh)
+__device__ __forceinline__ void app_win_load(const uint32_t* col, uint32_t b, uint32_t Z, uint32_t& lo, uint32_t& hi,
+                                             uint32_t& sh) {
+    b = min(b, b - Z);  // b mod Z (unsigned: b - Z wraps above b when b < Z)
+    lo = col[b >> 5];
+    hi = col[(b >> 5) + 1];
+    sh = b;
 }
 
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
@@ -488,6 +518,8 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
                 const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
+                // (a wave-uniform branch to the plain weights when no copy is unsatisfied, i.e. two versions
+                // of this loop, measured 15 % slower: code size)
                 const float x1 = !has_w ? mag : fmul(mag, (ucn && uf != 0.f) ? wu[k] : w[k]);
                 float x3;
                 if constexpr (KIND == NLDPC_MS) x3 = __builtin_amdgcn_fmed3f(x1, lo0, top);

@@ -12,8 +12,8 @@ for f in nldpc_graph.cpp nldpc_profile.cpp nldpc_forward.hip nldpc_backward.hip 
     cp -p $P/lib/obj/$f.o $OUT/obj/
 done
 cd $P/csrc
-env "$@" NLDPC_GEN_ONLY=bg2_z384 NLDPC_GEN_KINDS=3 python3 gen_fused.py $OUT/gen $R/resources
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function -fno-slp-vectorize -I$R/include -I$P/csrc"
+env NLDPC_GEN_ONLY=bg2_z384 NLDPC_GEN_KINDS=${KINDS:-3} "$@" python3 gen_fused.py $OUT/gen $R/resources
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function -fno-slp-vectorize -I$R/include -I$P/csrc ${EXTRA_FLAGS}"
 pids=""
 for g in $OUT/gen/*.hip; do
     b=$(basename $g)

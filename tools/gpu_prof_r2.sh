@@ -11,9 +11,9 @@ run() {  # name, timeout, rocprof args..., -- command
     echo "$name ok"
 }
 B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-sweep --no-count-only"
-run probe_fetch 120 --pmc FETCH_SIZE --kernel-trace -d $O/${TAG}_probe_fetch -o run --output-format csv -- python3 $R/tools/probe_pmc.py
-run probe_write 120 --pmc WRITE_SIZE --kernel-trace -d $O/${TAG}_probe_write -o run --output-format csv -- python3 $R/tools/probe_pmc.py
-for W in cfg3 cfg5; do
+[ -n "$NO_PROBE" ] || run probe_fetch 120 --pmc FETCH_SIZE --kernel-trace -d $O/${TAG}_probe_fetch -o run --output-format csv -- python3 $R/tools/probe_pmc.py
+[ -n "$NO_PROBE" ] || run probe_write 120 --pmc WRITE_SIZE --kernel-trace -d $O/${TAG}_probe_write -o run --output-format csv -- python3 $R/tools/probe_pmc.py
+for W in ${WORKLOADS:-cfg3 cfg5}; do
     run ${W}_trace 300 --kernel-trace --stats -d $O/${TAG}_${W}_trace -o run --output-format csv -- $B --workload $W
     run ${W}_fetch 300 --pmc FETCH_SIZE --kernel-trace -d $O/${TAG}_${W}_fetch -o run --output-format csv -- $B --workload $W --no-profile
     run ${W}_write 300 --pmc WRITE_SIZE --kernel-trace -d $O/${TAG}_${W}_write -o run --output-format csv -- $B --workload $W --no-profile

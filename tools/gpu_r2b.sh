@@ -20,4 +20,6 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print(f"cfg3ucn {sys.argv[2]:10s} {d['value']:>12.0f} cw/s  kernel {d['roofline']['avg_launch_ms']:.3f} ms")
 PY
 done
+[ -n "$NO_CFG5" ] || { timeout -k 10 600 python -u bench.py --workload cfg5 --steps 10 --warmup 3 > $O/${TAG}_bench_cfg5.log 2>&1 || exit $?;
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('cfg5', d['value'], 'cw/s', d['ms_per_step'], 'ms/step')" $O/${TAG}_bench_cfg5.log; }
 exit $rc
