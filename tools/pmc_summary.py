@@ -42,8 +42,11 @@ out["calibration"] = {
     "fetch_ratio_16B": fv[2] * 1024 / gib, "fetch_ratio_4B": fv[3] * 1024 / gib, "write_ratio": wv[1] * 1024 / gib,
 }
 KERNELS = {"cfg3": [("fused", "fused_bg2_z384::kernel<3, 0>", 65536)],
-           "cfg5": [("fused", "fused_bg2_z384::kernel<2, 1>", 2048), ("fusedb", "fusedb_bg2_z384::bwd_kernel<2>", 2048)]}
+           "cfg5": [("fused", "fused_bg2_z384::kernel<2, 1>", 2048), ("fusedb", "fusedb_bg2_z384::bwd_kernel<2>", 2048)],
+           "cfg3ucn": [("fused", "fused_bg2_z384::kernel<1, 0>", 65536)]}
 for w, ks in KERNELS.items():
+    if not os.path.isdir(os.path.join(root, f"{tag}_{w}_sq")):
+        continue
     f, _ = counters(f"{tag}_{w}_fetch")
     wr, _ = counters(f"{tag}_{w}_write")
     sq, sqdur = counters(f"{tag}_{w}_sq")
