@@ -54,8 +54,15 @@ __device__ __forceinline__ rsrc_t make_rsrc(const float* p, uint32_t bytes) {
 __device__ __forceinline__ float bload(rsrc_t r, uint32_t vo, int so) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
 }
+// Stores are non-temporal (cache-policy nt): the T posteriors stream out once and are never re-read by
+// the kernel, so they should not evict what is re-read from L2 -- the channel values of the Boosted
+// posterior with cumulative VN weights, and the descriptors' other lines.  Measured on MI355X: cfg3
+// Neural kernel 54.9 -> 51.7 ms, cfg3 Boosted MS NW(1,1,2) 116.4 -> 106.8 ms (profiles/r2_ab_boosted.txt).
+#ifndef NLDPC_STORE_AUX
+#define NLDPC_STORE_AUX 2
+#endif
 __device__ __forceinline__ void bstore(rsrc_t r, uint32_t vo, int so, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, so, NLDPC_STORE_AUX);
 }
 __device__ __forceinline__ void bstore8(rsrc_t r, uint32_t vo, int so, bool v) {
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, vo, so, 0);
