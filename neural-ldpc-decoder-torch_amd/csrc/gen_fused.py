@@ -88,6 +88,9 @@ for _item in filter(None, os.environ.get("NLDPC_GEN_GEOM", "").split(";")):
 XPRE = os.environ.get("NLDPC_GEN_XPRE", "2") == "1"
 XPRE2 = os.environ.get("NLDPC_GEN_XPRE", "2") == "2"
 
+# experiment knob: Neural check rows' copies 0 and 1 computed together, epilogue mul/add as packed f32
+CNPAIR2 = os.environ.get("NLDPC_GEN_CNPAIR2") == "1"
+
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
 
@@ -602,7 +605,16 @@ def emit(S: Spec) -> str:
                 if S.ucn_wave:
                     w("            }")
                 w("        }")
-                if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
+                pair_first = CNPAIR2 and CNPIPE and q == 0 and n + 1 < len(rcs) and rcs[n + 1] == (i, 1)
+                pair_second = CNPAIR2 and CNPIPE and q == 1
+                if "cnmath" in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
+                    pass
+                elif pair_first:  # Neural: copies 0 and 1 of the row together, packed epilogue
+                    w(f"        if constexpr (KIND == NLDPC_NEURAL) neural_row2<{DC}>(m{n}, m{n + 1}, wv, bv);")
+                    w(f"        else cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
+                elif pair_second:
+                    w(f"        if constexpr (KIND != NLDPC_NEURAL) cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
+                else:
                     w(f"        cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
                 for k, e in enumerate(es):
                     if e in d1set:

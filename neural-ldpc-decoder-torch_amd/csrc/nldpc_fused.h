@@ -280,6 +280,45 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
     }
 }
+// Two copies of one row (same weights) at once: the minimum tracking per copy as in neural_row, the
+// epilogue's |x|*w and + b as packed fp32 (v_pk_mul_f32 / v_pk_add_f32: per-lane IEEE, the same two
+// roundings as the scalar form).  Experiment (NLDPC_GEN_CNPAIR2).
+template <int DC>
+__device__ __forceinline__ void neural_row2(float (&ma)[DC], float (&mb)[DC], const float (&w)[DC], const float (&b)[DC]) {
+    float a1, a2, b1, b2;
+    two_smallest_abs<DC>(ma, a1, a2);
+    two_smallest_abs<DC>(mb, b1, b2);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(a1 == 0.f || b1 == 0.f) != 0, 0)) {
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            ma[k] = ma[k] == 0.f ? -20000.f : ma[k];
+            mb[k] = mb[k] == 0.f ? -20000.f : mb[k];
+        }
+        two_smallest_abs<DC>(ma, a1, a2);
+        two_smallest_abs<DC>(mb, b1, b2);
+    }
+    bool pa[DC], pb[DC];
+    bool para = false, parb = false;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        pa[k] = ma[k] > 0.f;
+        pb[k] = mb[k] > 0.f;
+        para ^= pa[k];
+        parb ^= pb[k];
+    }
+    float ag1 = __builtin_amdgcn_fmed3f(a1, 0.f, 10000.f), ag2 = __builtin_amdgcn_fmed3f(a2, 0.f, 10000.f);
+    float bg1 = __builtin_amdgcn_fmed3f(b1, 0.f, 10000.f), bg2 = __builtin_amdgcn_fmed3f(b2, 0.f, 10000.f);
+    asm volatile("" : "+v"(ag1), "+v"(ag2), "+v"(bg1), "+v"(bg2));
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const f2 mag = {fabsf(ma[k]) == a1 ? ag2 : ag1, fabsf(mb[k]) == b1 ? bg2 : bg1};
+        const f2 t = mag * f2{w[k], w[k]};
+        const f2 r = t + f2{b[k], b[k]};
+        const float ra = relu_mask(r.x), rb = relu_mask(r.y);
+        ma[k] = (para != pa[k]) ? ra : -ra;
+        mb[k] = (parb != pb[k]) ? rb : -rb;
+    }
+}
 #else
 template <int DC>
 __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
