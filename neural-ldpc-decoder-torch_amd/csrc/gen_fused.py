@@ -91,6 +91,10 @@ XPRE2 = os.environ.get("NLDPC_GEN_XPRE", "2") == "2"
 # experiment knob: Neural check rows' copies 0 and 1 computed together, epilogue mul/add as packed f32
 CNPAIR2 = os.environ.get("NLDPC_GEN_CNPAIR2") == "1"
 
+# check-row LDS addresses as 32-bit LDS byte offsets from one per-thread base (lu_ + constant: one
+# v_add_u32 per row copy instead of an add and a shift-add): cfg3 kernel 51.7 -> 50.9 ms (default 1; Neural and MS kernels only: QMS 169 -> 198 ms with it)
+ROADDR = os.environ.get("NLDPC_GEN_ROADDR", "1") == "1"
+
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
 
@@ -220,6 +224,8 @@ def emit(S: Spec) -> str:
     w("#define CNT (MODE >= 2)")
     w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
     w("#define D1_BYPASS (KIND == NLDPC_NEURAL && !SAVE)")
+    w("// check-row LDS addresses from one 32-bit base (ROADDR); in the QMS / SP kernels it measured slower")
+    w("#define ROA (KIND == NLDPC_NEURAL || KIND == NLDPC_MS)")
     w(f"#define UCNW (KIND == NLDPC_MS && {'true' if S.ucn_wave else 'false'})  // UCN bits by waves (Spec.ucn_wave)")
     assert NZ < 65536  # per-codeword error counts are packed two to an LDS word
 
@@ -537,6 +543,8 @@ def emit(S: Spec) -> str:
               f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps, "
               f"const uint32_t* appw) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
+            if ROADDR:
+                w("    const uint32_t lu_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u;")
             # row copies in order; weight offsets of each row in the preloaded W/Bv arrays
             rcs, woff, wo = [], {}, 0
             for i in S.cn_order[(p, ci)]:
@@ -550,13 +558,25 @@ def emit(S: Spec) -> str:
                 es = S.row_edges[i]
                 DC, e0 = len(es), es[0]
                 w(f"    float m{n}[{DC}];  // row {i} copy {q}")
-                w(f"    float* rq{n};")
-                w("    {")
-                w(f"        int ro = {(e0 - e0c) * Z + q * ZT} + u;  // one base VGPR per row copy: the edges ride in")
-                if not NORO:
-                    w("        asm volatile(\"\" : \"+v\"(ro));  // the 16-bit DS offset")
-                w(f"        rq{n} = lds + ro;")
-                w("    }")
+                if ROADDR:  # the row copy's LDS byte address = lu_ + constant: one v_add_u32 (ROA kinds)
+                    w(f"    std::conditional_t<ROA, lds_fp, float*> rq{n};")
+                    w("    if constexpr (ROA) {")
+                    w(f"        uint32_t rb = lu_ + {4 * ((e0 - e0c) * Z + q * ZT)}u;")
+                    w("        asm volatile(\"\" : \"+v\"(rb));")
+                    w(f"        rq{n} = (decltype(rq{n}))(uintptr_t)rb;")
+                    w("    } else {")
+                    w(f"        int ro = {(e0 - e0c) * Z + q * ZT} + u;")
+                    w("        asm volatile(\"\" : \"+v\"(ro));")
+                    w(f"        rq{n} = (decltype(rq{n}))(lds + ro);")
+                    w("    }")
+                else:
+                    w(f"    float* rq{n};")
+                    w("    {")
+                    w(f"        int ro = {(e0 - e0c) * Z + q * ZT} + u;  // one base VGPR per row copy: the edges ride in")
+                    if not NORO:
+                        w("        asm volatile(\"\" : \"+v\"(ro));  // the 16-bit DS offset")
+                    w(f"        rq{n} = lds + ro;")
+                    w("    }")
                 for k, e in enumerate(es):
                     if e in d1set:
                         w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = cd[{S.cd_index[p].index((e, q))}]; "
@@ -893,6 +913,7 @@ def emit(S: Spec) -> str:
     w("}")
     w("#undef D1_BYPASS")
     w("#undef UCNW")
+    w("#undef ROA")
     w("#undef SAVE")
     w("#undef CNT")
     w("#undef CM")

@@ -2,6 +2,8 @@
 // (gen_fused.py -> lib/gen/fused_*.hip) and their dispatcher in nldpc_forward.hip.
 #pragma once
 
+#include <type_traits>
+
 #include "nldpc_node.h"
 
 namespace nldpc {
@@ -168,6 +170,7 @@ __device__ __forceinline__ void app_win_load(const uint32_t* col, uint32_t b, ui
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
 // scalar loads (a row's edges are consecutive in C order: one s_load_dwordx8/x16 per row).
 typedef const float __attribute__((address_space(4)))* cfloat_p;
+typedef float __attribute__((address_space(3)))* lds_fp;  // LDS pointer (32-bit)
 
 // Neural check node of one check copy of a degree-DC row, in place: m[k] (gathered v2c) -> c2v, with
 // the reference's arithmetic (NeuralLDPCDecoder.py:74-91) specialised to what the Neural rule can
