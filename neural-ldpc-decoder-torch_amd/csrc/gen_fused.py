@@ -88,6 +88,9 @@ for _item in filter(None, os.environ.get("NLDPC_GEN_GEOM", "").split(";")):
 XPRE = os.environ.get("NLDPC_GEN_XPRE", "2") == "1"
 XPRE2 = os.environ.get("NLDPC_GEN_XPRE", "2") == "2"
 
+# check-node work balanced over the parts by (row, copy) units (1, default) or by whole rows (0)
+CNUNIT = os.environ.get("NLDPC_GEN_CNUNIT", "1") == "1"
+
 # experiment knob: Neural check rows' copies 0 and 1 computed together, epilogue mul/add as packed f32
 CNPAIR2 = os.environ.get("NLDPC_GEN_CNPAIR2") == "1"
 
@@ -166,6 +169,16 @@ class Spec:
         multi = [j for j in range(self.N) if deg(j) > 1]
         single = [j for j in range(self.N) if deg(j) == 1]
         self.reg_cols = balance(multi, deg, P)  # columns whose messages live in registers
+        # waves of a workgroup go round the 4 SIMDs, so with 2-wave parts the even parts share SIMDs
+        # {0,1} and the odd parts SIMDs {2,3}; the VN phase saturates the SIMDs, so order the parts
+        # for equal VN work (sequential adds per lane copy) on the two sets
+        if P == 8 and G * self.ZT == 128 and os.environ.get("NLDPC_GEN_SIMDBAL", "1") == "1":
+            import itertools
+            cost = [sum(deg(j) * (deg(j) - 1) // 2 + 2 * deg(j) + 1 for j in c) for c in self.reg_cols]
+            best = min(itertools.combinations(range(P), P // 2),
+                       key=lambda e: abs(sum(cost[k] for k in e) * 2 - sum(cost)))
+            odd = [k for k in range(P) if k not in best]
+            self.reg_cols = [self.reg_cols[k] for pair in zip(best, odd) for k in pair]
         self.d1_cols = balance(single, lambda j: 1, P)  # stateless degree-1 columns
         self.slots = [[e for j in cols_ for e in self.col_edges[j]] for cols_ in self.reg_cols]
         self.smax = max(1, max(len(s) for s in self.slots)) * Q
@@ -199,6 +212,25 @@ class Spec:
         self.nbuf = 2 if pipe else 1
         self.cn_rows = [balance(list(range(r0, r1)), lambda i: len(self.row_edges[i]), P)
                         for (r0, r1, _, _) in self.chunks]
+        # forward check-node work units (row i, lane copy q) of each chunk, balanced over the parts by
+        # degree (LPT): a row's Q copies may go to different parts.  A check-node phase is bound by
+        # its busiest wave (a chain of LDS round trips, one per row copy), and whole rows balanced
+        # badly: BG2 z=384 chunk 0 has 7 rows for 8 parts (edge copies per lane 30, 30, 24, 24, 18,
+        # 18, 12, 0; by units at most 21).  NLDPC_GEN_CNUNIT=0: whole rows (cn_rows)
+        if CNUNIT:
+            self.cn_units = []
+            for r0, r1, _, _ in self.chunks:
+                units = sorted(((i, q) for i in range(r0, r1) for q in range(Q)),
+                               key=lambda iq: (-len(self.row_edges[iq[0]]), iq[0], iq[1]))
+                load, bins = [0] * P, [[] for _ in range(P)]
+                for i, q in units:
+                    k = int(np.argmin(load))
+                    bins[k].append((i, q))
+                    load[k] += len(self.row_edges[i]) + 1  # + the row's fixed work
+                self.cn_units.append([sorted(b, key=lambda iq: (-len(self.row_edges[iq[0]]), iq[0], iq[1])) for b in bins])
+        else:
+            self.cn_units = [[[(i, q) for i in sorted(rows, key=lambda i: -len(self.row_edges[i])) for q in range(Q)]
+                              for rows in self.cn_rows[ci]] for ci in range(len(self.chunks))]
         self.lanes = G * self.ZT  # threads per part
         self.threads = P * self.lanes
         assert self.threads <= 1024 and self.lanes % 64 == 0, (tag, self.threads)
@@ -516,17 +548,16 @@ def emit(S: Spec) -> str:
     for p in range(S.P):
         lst = []
         for ci in range(len(S.chunks)):
-            for i in S.cn_rows[ci][p]:
+            for i, q in S.cn_units[ci][p]:
                 for e in S.row_edges[i]:
                     if e in d1set:
-                        for q in range(Q):
-                            lst.append((e, q))
+                        lst.append((e, q))
         S.cd_index[p] = lst
 
     S.cn_order, S.cn_nw = {}, {}
     for p in range(S.P):
         for ci in range(len(S.chunks)):
-            S.cn_order[(p, ci)] = sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i]))
+            S.cn_order[(p, ci)] = list(dict.fromkeys(i for i, _ in S.cn_units[ci][p]))  # distinct rows, unit order
             S.cn_nw[(p, ci)] = max(sum(len(S.row_edges[i]) for i in S.cn_order[(p, ci)]), 1)
 
     def rot(e, q):  # check copy h = u + q*ZT of edge e sits at variable copy (u + c) mod Z
@@ -546,12 +577,10 @@ def emit(S: Spec) -> str:
             if ROADDR:
                 w("    const uint32_t lu_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u;")
             # row copies in order; weight offsets of each row in the preloaded W/Bv arrays
-            rcs, woff, wo = [], {}, 0
+            rcs, woff, wo = list(S.cn_units[ci][p]), {}, 0
             for i in S.cn_order[(p, ci)]:
                 woff[i] = wo
                 wo += len(S.row_edges[i])
-                for q in range(Q):
-                    rcs.append((i, q))
 
             def rc_load(n):
                 i, q = rcs[n]
@@ -588,7 +617,7 @@ def emit(S: Spec) -> str:
                 i, q = rcs[n]
                 es = S.row_edges[i]
                 DC = len(es)
-                if S.ucn_wave and q == 0:
+                if S.ucn_wave and (n == 0 or rcs[n - 1][0] != i):  # the row's first unit in this part
                     # the row's unsatisfied flags for this wave's copies, all Q of them at once: lane 2q+h
                     # XORs the 32-bit windows (copies u0 + q*ZT + 32h + 0..31, rotated by each edge's shift)
                     # of the row's columns; the 2Q words become Q lane masks (bit l = lane l's flag)
@@ -745,9 +774,10 @@ def emit(S: Spec) -> str:
         chan_steps("s_", "            ")
         w("    }")
         def stamp(ph):
-            if STAMPS and len(S.chunks) == 2:
+            if STAMPS:
+                assert ph < 16
                 w(f"        if (a.stamps && blockIdx.x < 256 && (threadIdx.x & 63) == 0) "
-                  f"a.stamps[((blockIdx.x * {S.threads // 64} + (threadIdx.x >> 6)) * a.T + it) * 8 + {ph}] = "
+                  f"a.stamps[((blockIdx.x * {S.threads // 64} + (threadIdx.x >> 6)) * a.T + it) * 16 + {ph}] = "
                   f"__builtin_amdgcn_s_memtime();")
         # UCN: the hard-decision bit array of the codewords starts at zero (bits are OR-ed in); every later
         # iteration's array is cleared in the read-back phase of the iteration before
@@ -861,6 +891,7 @@ def emit(S: Spec) -> str:
             for k, ph in enumerate(phases):
                 for kind_, ci in ph:
                     {"w": op_w, "cn": op_cn, "r": op_r}[kind_](ci)
+                stamp(2 + k)  # arrival at the barrier that ends phase k (stamp 1: after the VN)
                 if k < len(phases) - 1:
                     w("        __syncthreads();")
             # a K-odd schedule ends with [R_{K-1}] alone after [R_{K-2}... ]: the next W0 (buffer 0) follows

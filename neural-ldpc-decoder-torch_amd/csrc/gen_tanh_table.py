@@ -14,8 +14,10 @@ evaluates.  Inputs whose double tanh lies within 8 double ulps of a fp32 halfway
 separately with their exact torch.tanh value, so the table does not depend on which double tanh
 the device uses.
 
-File layout (little-endian uint32): magic 0x4841544E ("NTAH"), version 1, SH, KMAX, n_entries,
-n_override; idx[(KMAX >> SH) + 2] (bucket b = key >> SH holds entries idx[b]..idx[b+1]);
+File layout (little-endian uint32): magic 0x4841544E ("NTAH"), version 2, SH, KMAX, n_entries,
+n_override; provenance[16] (64 bytes of NUL-padded ASCII: the torch version, ATen's CPU capability and
+the CPU model of the build host -- the table is what THAT torch.tanh computes; tests compare it with
+the torch of the machine they run on); idx[(KMAX >> SH) + 2] (bucket b = key >> SH holds entries idx[b]..idx[b+1]);
 entries[n_entries] = key | dir << 31, ascending in key (key = |x| bits; dir 1: torch.tanh is one ulp
 above the correctly rounded value, 0: one ulp below); overrides[n_override] = (key, result bits).
 
@@ -30,6 +32,17 @@ import torch
 
 SH = 15
 KMAX = int(np.float32(10.0).view(np.uint32))  # 0x41200000
+
+
+def provenance():
+    """torch version | ATen CPU capability | CPU model of this host (what the table was measured on)."""
+    cpu = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "?")
+    except OSError:
+        pass
+    return f"{torch.__version__}|{torch.backends.cpu.get_cpu_capability()}|{cpu}"
 
 
 def main(out):
@@ -61,7 +74,7 @@ def main(out):
     nb = (KMAX >> SH) + 2
     idx = np.searchsorted(keys, (np.arange(nb, dtype=np.uint64) << np.uint64(SH)).astype(np.uint32)).astype(np.uint32)
     idx[-1] = len(ent)
-    hdr = struct.pack("<6I", 0x4841544E, 1, SH, KMAX, len(ent), len(overrides))
+    hdr = struct.pack("<6I", 0x4841544E, 2, SH, KMAX, len(ent), len(overrides)) + provenance().encode()[:63].ljust(64, b"\0")
     tmp = out + ".tmp"
     with open(tmp, "wb") as f:
         f.write(hdr)

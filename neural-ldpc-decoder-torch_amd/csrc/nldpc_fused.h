@@ -40,7 +40,7 @@ struct FusedArgs {
     const uint8_t* cnt_y;  // [B][N][Z] codeword bits (MODE 3), or nullptr (all-zero codeword, MODE 2)
     int32_t cnt_conv;      // 0: bit = LLR > 0; 1: bit = LLR < 0
     unsigned long long* cnt;  // [T][2] (+=) bit errors, frame errors
-    uint64_t* stamps;    // diagnostic stamp build only (make STAMPS=1): [256][waves][T][8] s_memtime
+    uint64_t* stamps;    // diagnostic stamp build only (make STAMPS=1): [256][waves][T][16] s_memtime
 };
 
 // Global memory of the fused kernels goes through buffer descriptors built from wave-uniform values:

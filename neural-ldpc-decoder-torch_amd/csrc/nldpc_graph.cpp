@@ -62,7 +62,8 @@ TanhRef tanh_ref_table(int device) {
     std::vector<uint32_t> buf;
     if (FILE* f = std::fopen(tanh_table_path().c_str(), "rb")) {
         uint32_t h[6];
-        if (std::fread(h, 4, 6, f) == 6 && h[0] == 0x4841544Eu && h[1] == 1u) {
+        uint32_t prov[16];  // version 2: 64 bytes of build-host provenance (gen_tanh_table.py), not used here
+        if (std::fread(h, 4, 6, f) == 6 && h[0] == 0x4841544Eu && (h[1] == 1u || (h[1] == 2u && std::fread(prov, 4, 16, f) == 16))) {
             const size_t nidx = (h[3] >> h[2]) + 2, n = nidx + h[4] + 2 * (size_t)h[5];
             buf.resize(n);
             if (std::fread(buf.data(), 4, n, f) == n) {

@@ -36,7 +36,7 @@ struct DevGraph {
     TanhRef tanh;
 };
 // the process-wide device copy of lib/nldpc_tanh_ref.bin for `device` (loaded once; idx == nullptr
-// when the file is missing: SP decodes then fail with NLDPC_EUNSUPPORTED)
+// when the file is missing: the SP check node then uses the rounded double tanh, within one ulp)
 TanhRef tanh_ref_table(int device);
 
 }  // namespace nldpc

@@ -24,7 +24,7 @@ namespace nldpc {
 __device__ __noinline__ float tanh_ref(float x, TanhRef t) {
     const uint32_t key = __float_as_uint(x) & 0x7fffffffu;
     uint32_t r = __float_as_uint((float)tanh((double)__uint_as_float(key)));
-    if (key <= t.kmax) {
+    if (t.idx && key <= t.kmax) {  // no table (lib/nldpc_tanh_ref.bin missing): the rounded double tanh
         const uint32_t b = key >> t.sh;
         uint32_t lo = t.idx[b], hi = t.idx[b + 1];
         const uint32_t end = hi;

@@ -44,12 +44,22 @@ def _tanh_table():
             _tanh_tab = False
         else:
             raw = np.fromfile(_TANH_BIN, dtype=np.uint32)
-            _, _, sh, kmax, n, nov = (int(v) for v in raw[:6])
+            _, ver, sh, kmax, n, nov = (int(v) for v in raw[:6])
+            h = 6 + (16 if ver >= 2 else 0)  # version 2: 64 bytes of build-host provenance
             nidx = (kmax >> sh) + 2
-            ent = raw[6 + nidx:6 + nidx + n]
-            ov = raw[6 + nidx + n:6 + nidx + n + 2 * nov].reshape(-1, 2)
+            ent = raw[h + nidx:h + nidx + n]
+            ov = raw[h + nidx + n:h + nidx + n + 2 * nov].reshape(-1, 2)
             _tanh_tab = ((ent & 0x7FFFFFFF).astype(np.int64), (ent >> 31).astype(np.int64), ov.astype(np.int64), kmax)
     return _tanh_tab or None
+
+
+def tanh_table_provenance():
+    """'torch version|CPU capability|CPU model' of the host that built lib/nldpc_tanh_ref.bin (version 2
+    tables), '' for a version 1 table, None when there is no table."""
+    if not os.path.exists(_TANH_BIN):
+        return None
+    raw = np.fromfile(_TANH_BIN, dtype=np.uint32, count=22)
+    return raw[6:22].tobytes().split(b"\0")[0].decode() if int(raw[1]) >= 2 else ""
 
 
 def _tanh(x: torch.Tensor) -> torch.Tensor:

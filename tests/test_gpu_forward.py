@@ -1,7 +1,6 @@
 """GPU parity of the forward decode (HIP kernels through the C ABI) against the reference's golden
 outputs and the CPU oracle.  Neural / MS / QMS: bit-exact soft outputs; SP: hard decisions exact and
-soft values within SURVEY §8(c) C3's SP tolerance, rtol 1e-4 / atol 2e-3, with no outlier allowance
-(sp_check).
+soft values within the north star's 1e-4 relative and, beyond that, value for value (sp_check).
 """
 import glob
 import os
@@ -20,11 +19,25 @@ DEV = torch.device("cuda")
 
 
 def sp_check(o, ref):
-    """SP parity (north star 1e-4 relative): equal hard decisions, every soft value
-    within rtol 1e-4 / atol 2e-3 of the reference (or of the oracle, which reproduces the reference's
-    SP bit for bit: tests/test_oracle_golden.py)."""
+    """SP parity (north star: hard decisions bit-exact, soft values within 1e-4 RELATIVE): equal hard
+    decisions and every soft value within rtol 1e-4 of the reference (or of the oracle, which
+    reproduces the reference's SP bit for bit: tests/test_oracle_golden.py), with no absolute
+    allowance.  The number of values that are not identical is reported (NLDPC_SP_LOG=<file> appends
+    one line per check): the device SP follows ATen's product order and torch.tanh's recorded values,
+    so against the fixtures (made on this container's torch) and against the oracle (same table) it is
+    value for value, and the check asserts that after the 1e-4 bound."""
+    o, ref = np.asarray(o), np.asarray(ref)
     assert np.array_equal(o > 0, ref > 0), f"{((o > 0) != (ref > 0)).sum()} hard decisions differ"
-    np.testing.assert_allclose(o, ref, rtol=1e-4, atol=2e-3)
+    ndiff = int((o != ref).sum())
+    rel = float(np.max(np.abs(o - ref) / np.maximum(np.abs(ref), 1e-30))) if ndiff else 0.0
+    log = os.environ.get("NLDPC_SP_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(f"{os.environ.get('PYTEST_CURRENT_TEST', '?').split(' ')[0]} values {o.size} not_identical {ndiff} "
+                    f"max_rel {rel:.3e}\n")
+    np.testing.assert_allclose(o, ref, rtol=1e-4, atol=0)
+    assert ndiff == 0, f"{ndiff} of {o.size} SP soft values within 1e-4 but not identical (max rel {rel:.2e})"
+    return ndiff
 
 
 def _bg(name):
@@ -359,3 +372,32 @@ def test_lifting_96_fused_matches_oracle(kind):
         ref = torch.stack([r[t] for t in range(T)]).numpy()
     o = outs.cpu().numpy()
     assert np.array_equal(o, ref), f"{(o != ref).sum()} of {o.size} differ"
+
+
+def test_tanh_table_vs_this_hosts_torch():
+    """The SP check node's torch.tanh values (lib/nldpc_tanh_ref.bin, recorded by gen_tanh_table.py on
+    the machine the fixtures were made on; provenance in its header) against THIS machine's
+    torch.tanh.  The device and the oracle both use the table, so SP parity with the fixtures holds on
+    any host; what this measures is how far this host's own torch.tanh (the one a reference run here
+    would call) is from it: MKL's vector tanh takes host-dependent code paths, each within one ulp of
+    the correctly rounded tanh.  Asserted: at most one ulp everywhere; the number of differing values
+    is reported (NLDPC_SP_LOG), and a host that needs value-for-value parity with ITS torch rebuilds
+    the table there (python3 csrc/gen_tanh_table.py <file>; NLDPC_TANH_TABLE=<file>)."""
+    from oracle import ldpc_oracle as lo
+    tab = lo._tanh_table()
+    assert tab is not None, "lib/nldpc_tanh_ref.bin is missing next to libnldpc.so"
+    here = f"{torch.__version__}|{torch.backends.cpu.get_cpu_capability()}"
+    gen = torch.Generator().manual_seed(12)
+    x = torch.cat([(torch.rand(1 << 20, generator=gen) * 20 - 10),
+                   torch.from_numpy(tab[0][::37].astype(np.int32)).view(torch.float32)])
+    x = torch.cat([x, -x])
+    got, want = lo._tanh(x), torch.tanh(x)
+    ulps = (got.view(torch.int32).long() - want.view(torch.int32).long()).abs()
+    bad = int((ulps != 0).sum())
+    msg = (f"{bad} of {x.numel()} tanh values differ (max {int(ulps.max())} ulp): table built on "
+           f"'{lo.tanh_table_provenance()}', this host '{here}'")
+    log = os.environ.get("NLDPC_SP_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(f"tanh table vs this host's torch.tanh: {msg}\n")
+    assert int(ulps.max()) <= 1, msg
