@@ -55,6 +55,9 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    # (test hook) gloo: the rank processes may share a GPU (cuda:rank % device_count) -- the product's
+    # rank launch, sharding, counter all-reduce and max-time run on the one-GPU test box
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl", help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
@@ -231,10 +234,10 @@ def main():
     if rc is not None:
         sys.exit(rc)
     from nldpc import distributed as nd_dist
-    rank, world, local = nd_dist.init("nccl")
+    rank, world, local = nd_dist.init(args.backend)
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but {world} rank(s) are running")
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local if args.backend == "nccl" else local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     gfile, Z, T, B = WORKLOADS[args.workload]
     T = args.iters or T

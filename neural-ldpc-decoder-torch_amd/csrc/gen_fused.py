@@ -38,9 +38,10 @@ def app_words(N, Z):
     return N * ((Z + 31) // 32 + 1)
 # check rows up to this degree let the compiler interleave their lane copies (more ILP, more registers)
 CN_PAIR_MAXDC = int(os.environ.get("NLDPC_GEN_CNPAIR", "0"))
-# VN lane copies as packed fp32 pairs (v_pk_add_f32) or all scalar chains.  Measured on gfx950 (stamp
-# build): a v_pk_add_f32 occupies the SIMD for 8 cycles against 2 for v_add_f32, so packing costs
-# time per element; scalar is the default
+# VN lane copies as packed fp32 pairs (v_pk_add_f32) or all scalar chains.  Measured on gfx950
+# (tools/dev/valu_rate2.hip, profiles/r3_valu_rate2.txt): v_add_f32 issues every 2 cycles per SIMD at
+# >= 2 waves, v_pk_add_f32 every 4 -- the same adds per cycle, so packing buys nothing and costs the
+# register pairs; scalar is the default
 PACK_VN = os.environ.get("NLDPC_GEN_PACK") == "1"
 PACK_MAX = int(os.environ.get("NLDPC_GEN_PACKMAX", "0"))
 # experiment knob: no opaque row base in the check-node phase (lets the compiler prove the row copies'
@@ -87,6 +88,13 @@ for _item in filter(None, os.environ.get("NLDPC_GEN_GEOM", "").split(";")):
 # each column (slower: 124 -> 130 ms); 0 = next to each posterior
 XPRE = os.environ.get("NLDPC_GEN_XPRE", "2") == "1"
 XPRE2 = os.environ.get("NLDPC_GEN_XPRE", "2") == "2"
+
+# experiment knob: the lanes of a wrapped copy (own / rot) pick their address by a scalar-computed lane
+# mask (1) instead of a per-lane compare and select (0, default).  On gfx950 v_cmp / v_cndmask issue at
+# half the rate of v_add_f32 (tools/dev/valu_rate2.hip, profiles/r3_valu_rate2*.txt), but the 64-bit
+# masks pushed the kernel's SGPRs (weights of two chunks in flight) into spills: cfg3 49.1 -> 51.3 ms
+# (profiles/r3_ab_cn.txt)
+WRAPMASK = os.environ.get("NLDPC_GEN_WRAPMASK", "0") == "1"
 
 # check-node work balanced over the parts by (row, copy) units (1, default) or by whole rows (0)
 CNUNIT = os.environ.get("NLDPC_GEN_CNUNIT", "1") == "1"
@@ -243,6 +251,8 @@ def emit(S: Spec) -> str:
     L = []
     w = L.append
     CF = S.chunk_floats
+    # wrapped lane copies by scalar lane masks (own_lv): needs waves of 64 consecutive copies of one codeword
+    WRAPM = WRAPMASK and G == 1 and ZT % 64 == 0
     w(f"// ---- {S.tag}: M={S.M} N={S.N} E={S.E} Z={Z}; workgroup = {G} codeword(s) x {S.P} part(s) x {ZT} lanes "
       f"= {S.threads} threads, {Q} cop{'y' if Q == 1 else 'ies'} per lane; register slots/part "
       f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B")
@@ -477,6 +487,26 @@ def emit(S: Spec) -> str:
             return f"{base} + u"
         return f"{base} + u - (u >= {Z - cq} ? {Z} : 0)"
 
+    def own_lv(e, q, e0):
+        """The LDS element own() indexes, as an lvalue.  WRAPM: a wrapped copy's lanes pick between two
+        per-thread byte bases (lu0_, lu1_ = lu0_ - 4Z) by a lane mask the scalar unit computes from the
+        wave's first copy (wrap_mask), one v_cndmask instead of a compare, a select and an add."""
+        cq = (q * ZT - int(S.shift[e])) % Z
+        base = (e - e0) * Z + cq
+        if cq + ZT <= Z or not WRAPM:
+            return f"lds[{own(e, q, e0)}]"
+        return (f"((lds_fp)(uintptr_t)((__builtin_amdgcn_inverse_ballot_w64(wrap_mask({Z - cq}, u0_)) ? lu1_ : lu0_) "
+                f"+ {4 * base}u))[0]")
+
+    def wrap_u0():  # before the asm barrier on u, so the compiler computes it once, not per phase
+        if WRAPM:
+            w("    const int u0_ = __builtin_amdgcn_readfirstlane(u) & ~63;  // the wave's first lane copy")
+
+    def wrap_prelude():
+        if WRAPM:
+            w("    const uint32_t lu0_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u, lu1_ = lu0_ - "
+              f"{4 * Z}u;")
+
     for p in range(S.P):
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
             mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
@@ -484,17 +514,19 @@ def emit(S: Spec) -> str:
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void wr_p{p}_c{ci}({state_params(p, True)}, {x_params(p)}, float* lds, "
               f"int u, const FusedArgs& a, int it, rsrc_t sv, uint32_t vc) {{")
+            wrap_u0()
             w("    asm volatile(\"\" : \"+v\"(u));  // LDS addresses are recomputed here, not hoisted out of the loop")
+            wrap_prelude()
             for q in range(Q):
                 for k, e in mine:
-                    w(f"    lds[{own(e, q, e0)}] = {ref(p, q, k)};")
+                    w(f"    {own_lv(e, q, e0)} = {ref(p, q, k)};")
                     w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(p, q, k)}, a.qbit);")
             if d1:  # v2c = (0 + xin) + 0: no other edge in the column (bypass: the check node reads xa)
                 w("    if constexpr (!D1_BYPASS) {")
             for j, e in d1:
                 for q in range(Q):
                     w(f"    {{ const float v_ = fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f); "
-                      f"lds[{own(e, q, e0)}] = v_; if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qbit); }}")
+                      f"{own_lv(e, q, e0)} = v_; if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qbit); }}")
             if d1:
                 w("    }")
             w("}")
@@ -502,10 +534,12 @@ def emit(S: Spec) -> str:
             w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
               f"int u, const FusedArgs& a, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co, "
               f"uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t& d1m) {{")
+            wrap_u0()
             w("    asm volatile(\"\" : \"+v\"(u));")
+            wrap_prelude()
             for q in range(Q):
                 for k, e in mine:
-                    w(f"    {ref(p, q, k)} = lds[{own(e, q, e0)}];")
+                    w(f"    {ref(p, q, k)} = {own_lv(e, q, e0)};")
             if d1:  # this iteration's posterior right away (bypass: written by the check node)
                 w("    if constexpr (!D1_BYPASS) {")
             if XPRE2:
@@ -519,7 +553,7 @@ def emit(S: Spec) -> str:
                         w(f"    {{ const float xo_ = xl_{j}_{q};")
                     else:
                         w(f"    {{ const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
-                    w(f"      const float P_ = fadd(0.f, lds[{own(e, q, e0)}]);")
+                    w(f"      const float P_ = fadd(0.f, {own_lv(e, q, e0)});")
                     w("      float y_;")
                     w("      if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w(f"          bool m_; y_ = posterior_m<KIND>(xo_, P_, a, m_); bstore(pr, vo, {X(j, q)}, y_); "
@@ -530,7 +564,7 @@ def emit(S: Spec) -> str:
                 w("    if (has_co) {  // final message state (last iteration only)")
                 for j, e in d1:
                     for q in range(Q):
-                        w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, lds[{own(e, q, e0)}]);")
+                        w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, {own_lv(e, q, e0)});")
                 w("    }")
                 w("    }")
             w("}")
@@ -560,10 +594,13 @@ def emit(S: Spec) -> str:
             S.cn_order[(p, ci)] = list(dict.fromkeys(i for i, _ in S.cn_units[ci][p]))  # distinct rows, unit order
             S.cn_nw[(p, ci)] = max(sum(len(S.row_edges[i]) for i in S.cn_order[(p, ci)]), 1)
 
-    def rot(e, q):  # check copy h = u + q*ZT of edge e sits at variable copy (u + c) mod Z
+    def rot(e, q, mask=False):  # check copy h = u + q*ZT of edge e sits at variable copy (u + c) mod Z
         c = (q * ZT + int(S.shift[e])) % Z
-        dv = f"(u >= {Z - c} ? {(-4 * Z) & 0xFFFFFFFF}u : 0u)" if c + ZT > Z else "0u"
-        return c, dv
+        if c + ZT <= Z:
+            return c, "0u"
+        if mask and WRAPM:  # (check-node phase: u0_ defined, see own_lv)
+            return c, f"(__builtin_amdgcn_inverse_ballot_w64(wrap_mask({Z - c}, u0_)) ? {(-4 * Z) & 0xFFFFFFFF}u : 0u)"
+        return c, f"(u >= {Z - c} ? {(-4 * Z) & 0xFFFFFFFF}u : 0u)"
 
     for p in range(S.P):
         ncd = max(len(S.cd_index[p]), 1)
@@ -573,6 +610,7 @@ def emit(S: Spec) -> str:
               f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last, "
               f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps, "
               f"const uint32_t* appw) {{")
+            wrap_u0()
             w("    asm volatile(\"\" : \"+v\"(u));")
             if ROADDR:
                 w("    const uint32_t lu_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u;")
@@ -668,7 +706,7 @@ def emit(S: Spec) -> str:
                 for k, e in enumerate(es):
                     if e in d1set:
                         j = int(S.hb_cols[e])
-                        c, dv = rot(e, q)
+                        c, dv = rot(e, q, mask=True)
                         w("        if constexpr (D1_BYPASS) {")
                         w(f"            const uint32_t dv_ = {dv};")
                         w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, "

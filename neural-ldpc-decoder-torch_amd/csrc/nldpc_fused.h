@@ -167,10 +167,26 @@ __device__ __forceinline__ void app_win_load(const uint32_t* col, uint32_t b, ui
     sh = b;
 }
 
+// Lanes l of a wave (copies u0 + l, u0 = the wave's first copy) with u0 + l >= T, as a lane mask: all
+// scalar arithmetic on wave-uniform values (the generated code's wrapped copies, gen_fused.py own_lv)
+__device__ __forceinline__ uint64_t wrap_mask(int T, int u0) {
+    const int sh = T - u0;
+    return sh <= 0 ? ~0ull : (sh >= 64 ? 0ull : (~0ull << sh));
+}
+
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
 // scalar loads (a row's edges are consecutive in C order: one s_load_dwordx8/x16 per row).
 typedef const float __attribute__((address_space(4)))* cfloat_p;
 typedef float __attribute__((address_space(3)))* lds_fp;  // LDS pointer (32-bit)
+
+// NLDPC_CMIN: the min / max / median helpers below as plain C (fminf, fabsf, __builtin_amdgcn_fmed3f)
+// for a translation unit compiled with -mno-amdgpu-ieee -fno-honor-nans (the generated kernels: the
+// decoder's values are never NaN), where the compiler needs no canonicalising v_max per operand and folds
+// |x| into the source modifiers itself; the inline-asm forms (IEEE mode) are opaque to its hazard
+// recognizer, which pads them with s_nop, and to its scheduler.
+#ifndef NLDPC_CMIN
+#define NLDPC_CMIN 0
+#endif
 
 // Neural check node of one check copy of a degree-DC row, in place: m[k] (gathered v2c) -> c2v, with
 // the reference's arithmetic (NeuralLDPCDecoder.py:74-91) specialised to what the Neural rule can
@@ -187,9 +203,13 @@ typedef float __attribute__((address_space(3)))* lds_fp;  // LDS pointer (32-bit
 // on gfx950 against a log-depth tournament (pairs, then merges of 3-4 ops): 6 % fewer SIMD cycles per
 // row copy at 4 waves per SIMD (tools/dev/cn_micro.hip) -- the other waves cover the serial chain.
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+#if NLDPC_CMIN
+    return max(min(a, b), min(max(a, b), c));  // (the compiler forms v_med3_u32)
+#else
     uint32_t d;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
+#endif
 }
 
 template <int DC>
@@ -213,24 +233,40 @@ __device__ __forceinline__ void two_smallest(const uint32_t (&key)[DC], uint32_t
 // asm: written as fminf/fmaxf the compiler materialises every fabsf (v_and_b32) and, in IEEE mode,
 // canonicalises each operand (v_max_f32 x, x) -- three extra VALU per edge.  Plain VALU, no hazards.
 __device__ __forceinline__ float min_aa(float x, float y) {
+#if NLDPC_CMIN
+    return fminf(fabsf(x), fabsf(y));
+#else
     float d;
     asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(d) : "v"(x), "v"(y));
     return d;
+#endif
 }
 __device__ __forceinline__ float max_aa(float x, float y) {
+#if NLDPC_CMIN
+    return fmaxf(fabsf(x), fabsf(y));
+#else
     float d;
     asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(d) : "v"(x), "v"(y));
     return d;
+#endif
 }
 __device__ __forceinline__ float min_a(float a, float x) {  // min(a, |x|), a >= 0
+#if NLDPC_CMIN
+    return fminf(a, fabsf(x));
+#else
     float d;
     asm("v_min_f32_e64 %0, %1, |%2|" : "=v"(d) : "v"(a), "v"(x));
     return d;
+#endif
 }
 __device__ __forceinline__ float med3_a(float a, float b, float x) {  // med3(a, b, |x|)
+#if NLDPC_CMIN
+    return __builtin_amdgcn_fmed3f(a, b, fabsf(x));
+#else
     float d;
     asm("v_med3_f32 %0, %1, %2, |%3|" : "=v"(d) : "v"(a), "v"(b), "v"(x));
     return d;
+#endif
 }
 
 template <int DC>
@@ -250,6 +286,79 @@ __device__ __forceinline__ void two_smallest_abs(const float (&m)[DC], float& mi
     }
 }
 
+// The two smallest of |m_k| (as a multiset) with three-input min / median: the first three by one
+// v_min3 + one v_med3, then two more at a time by three ops -- with a <= b the running pair,
+// a' = min3(a, |x|, |y|), b' = min(b, med3(a, |x|, |y|)) -- and a last single one by med3 + min:
+// 1.5 ops per element instead of 2 (on gfx950 min / max / med3 all issue at half the v_add_f32 rate,
+// profiles/r3_valu_rate2*.txt).  CAP: the reference's masked tile entries (10000) take part as one
+// more element, so the minima come out capped (for an even DC that costs one op instead of two clamps).
+__device__ __forceinline__ float min3_aaa(float x, float y, float z) {
+#if NLDPC_CMIN
+    return fminf(fminf(fabsf(x), fabsf(y)), fabsf(z));
+#else
+    float d;
+    asm("v_min3_f32 %0, |%1|, |%2|, |%3|" : "=v"(d) : "v"(x), "v"(y), "v"(z));
+    return d;
+#endif
+}
+__device__ __forceinline__ float med3_aaa(float x, float y, float z) {
+#if NLDPC_CMIN
+    return __builtin_amdgcn_fmed3f(fabsf(x), fabsf(y), fabsf(z));
+#else
+    float d;
+    asm("v_med3_f32 %0, |%1|, |%2|, |%3|" : "=v"(d) : "v"(x), "v"(y), "v"(z));
+    return d;
+#endif
+}
+__device__ __forceinline__ float min3_ra(float a, float x, float y) {  // min3(a, |x|, |y|)
+#if NLDPC_CMIN
+    return fminf(fminf(a, fabsf(x)), fabsf(y));
+#else
+    float d;
+    asm("v_min3_f32 %0, %1, |%2|, |%3|" : "=v"(d) : "v"(a), "v"(x), "v"(y));
+    return d;
+#endif
+}
+__device__ __forceinline__ float med3_ra(float a, float x, float y) {  // med3(a, |x|, |y|)
+#if NLDPC_CMIN
+    return __builtin_amdgcn_fmed3f(a, fabsf(x), fabsf(y));
+#else
+    float d;
+    asm("v_med3_f32 %0, %1, |%2|, |%3|" : "=v"(d) : "v"(a), "v"(x), "v"(y));
+    return d;
+#endif
+}
+__device__ __forceinline__ float min_rr(float a, float b) {  // v_min_f32 without fminf's canonicalising v_max
+#if NLDPC_CMIN
+    return fminf(a, b);
+#else
+    float d;
+    asm("v_min_f32_e32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+#endif
+}
+template <int DC, bool CAP>
+__device__ __forceinline__ void two_smallest_abs3(const float (&m)[DC], float& min1, float& min2) {
+    constexpr int n = DC + (CAP ? 1 : 0);
+    static_assert(n >= 3, "two_smallest_abs3 needs three elements");
+    const float cap = 10000.f;
+    auto el = [&](int k) { return k < DC ? m[k] : cap; };  // the cap (positive) is its own |x|
+    float a = min3_aaa(el(0), el(1), el(2)), b = med3_aaa(el(0), el(1), el(2));
+    int k = 3;
+#pragma unroll
+    for (; k + 1 < n; k += 2) {
+        const float md = med3_ra(a, el(k), el(k + 1));
+        a = min3_ra(a, el(k), el(k + 1));
+        b = min_rr(b, md);
+    }
+    if (k < n) {
+        b = med3_a(a, b, el(k));
+        a = min_a(a, el(k));
+    }
+    min1 = a;
+    min2 = b;
+}
+
 #ifndef NLDPC_CN_KEYS
 // Float-domain form (default): per edge two min-tracking ops, the argmin compare with |m_k| as a
 // modifier, the epilogue and the sign -- no per-edge key and no per-row key decode.  Exact zeros
@@ -257,15 +366,54 @@ __device__ __forceinline__ void two_smallest_abs(const float (&m)[DC], float& mi
 // after iteration 0; a row copy in which any lane of the wave sees one (min1 == 0) takes a
 // wave-uniform branch that maps each 0 to -20000 (magnitude above the 10000 clamp, not positive) and
 // tracks the minimum again.  Bit-identical to the key form below (-DNLDPC_CN_KEYS) and to cn_core.
+#ifndef NLDPC_CN_MIN3
+#define NLDPC_CN_MIN3 1
+#endif
+#ifndef NLDPC_CN_XSIGN
+#define NLDPC_CN_XSIGN 0
+#endif
 template <int DC>
 __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
-    float min1, min2;
-    two_smallest_abs<DC>(m, min1, min2);
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(min1 == 0.f) != 0, 0)) {
+    float min1, min2, mg1, mg2;
+    if constexpr (NLDPC_CN_MIN3 && DC >= 3) {
+        // the minima capped at 10000 inside the tracking (even DC) or by one min each (odd DC)
+        constexpr bool cap = DC % 2 == 0;
+        two_smallest_abs3<DC, cap>(m, min1, min2);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(min1 == 0.f) != 0, 0)) {
 #pragma unroll
-        for (int k = 0; k < DC; ++k) m[k] = m[k] == 0.f ? -20000.f : m[k];
+            for (int k = 0; k < DC; ++k) m[k] = m[k] == 0.f ? -20000.f : m[k];
+            two_smallest_abs3<DC, cap>(m, min1, min2);
+        }
+        mg1 = cap ? min1 : min_rr(min1, 10000.f);
+        mg2 = cap ? min2 : min_rr(min2, 10000.f);
+    } else {
         two_smallest_abs<DC>(m, min1, min2);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(min1 == 0.f) != 0, 0)) {
+#pragma unroll
+            for (int k = 0; k < DC; ++k) m[k] = m[k] == 0.f ? -20000.f : m[k];
+            two_smallest_abs<DC>(m, min1, min2);
+        }
+        mg1 = __builtin_amdgcn_fmed3f(min1, 0.f, 10000.f);  // the masked tile entries (10000) take part
+        mg2 = __builtin_amdgcn_fmed3f(min2, 0.f, 10000.f);  // in the min (min1, min2 >= 0: a clamp)
     }
+#if NLDPC_CN_XSIGN
+    // sign by bit arithmetic (m has no zeros here): the output is positive iff the number of positive
+    // OTHER inputs is odd, i.e. its sign bit is sb_k ^ (xor of all sign bits) ^ (DC & 1) -- one v_xor per
+    // edge into the row's sign word and one bit insert per edge, instead of a compare into a lane
+    // mask and a select (both half-rate on gfx950); no lane masks held in SGPRs
+    uint32_t xs = (DC & 1) ? 0x80000000u : 0u;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) xs ^= __float_as_uint(m[k]);
+    asm volatile("" : "+v"(mg1), "+v"(mg2));
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
+        const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
+        // r = max(., 0) is +0 or positive (or -0, whose sign bit the OR leaves set: a zero's sign is
+        // never observed by the decoder's sums)
+        m[k] = __uint_as_float(__float_as_uint(r) | ((__float_as_uint(m[k]) ^ xs) & 0x80000000u));
+    }
+#else
     bool pos[DC];
     bool par = false;
 #pragma unroll
@@ -273,8 +421,6 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         pos[k] = m[k] > 0.f;
         par ^= pos[k];
     }
-    float mg1 = __builtin_amdgcn_fmed3f(min1, 0.f, 10000.f);  // the masked tile entries (10000) take part
-    float mg2 = __builtin_amdgcn_fmed3f(min2, 0.f, 10000.f);  // in the min (min1, min2 >= 0: a clamp)
     asm volatile("" : "+v"(mg1), "+v"(mg2));
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
@@ -282,6 +428,7 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
         m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
     }
+#endif
 }
 // Two copies of one row (same weights) at once: the minimum tracking per copy as in neural_row, the
 // epilogue's |x|*w and + b as packed fp32 (v_pk_mul_f32 / v_pk_add_f32: per-lane IEEE, the same two
@@ -533,7 +680,8 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
                                             float hi, bool ucn, float uf, const float (&wu)[DC]) {
     if constexpr (DC >= 2) {
         float min1, min2;
-        two_smallest_abs<DC>(m, min1, min2);
+        if constexpr (NLDPC_CN_MIN3 && DC >= 3) two_smallest_abs3<DC, false>(m, min1, min2);
+        else two_smallest_abs<DC>(m, min1, min2);
         bool fast = true;
         if constexpr (KIND == NLDPC_MS)
             fast = lo == -hi && hi > kZeroFix && __builtin_amdgcn_ballot_w64(min1 <= kZeroFix) == 0;

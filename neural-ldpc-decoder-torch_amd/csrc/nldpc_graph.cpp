@@ -89,6 +89,11 @@ TanhRef tanh_ref_table(int device) {
 // ascending p --, combines each lane as (a0*a1)*(a2*a3), the lanes left to right, then multiplies the
 // remaining positions one by one.  Factors of exactly 1.0 change nothing, so only the row's own edges
 // matter: per row, its edges sorted by (lane, accumulator, position), tail positions last.
+// The lane width (8) is what ATen's reduction used on the machine the SP fixtures were made on (this
+// container: torch 2.10.0+rocm7.0, CPU capability AVX512, measured by
+// tests/test_oracle_golden.py::test_prod_order_model_matches_torch_prod); the order is a property of
+// that ATen build, and a host whose ATen vectorises the product differently needs another plan (the
+// device SP then stays within the SP tolerance of that host's torch, but not value for value).
 static void sp_plans(int M, int E, const std::vector<int32_t>& chk, const std::vector<int32_t>& var,
                      const std::vector<int32_t>& row_ptr, std::vector<uint8_t>& plan) {
     std::vector<int32_t> vorder(E), vidx(E);

@@ -15,9 +15,15 @@ What is different from the reference and why:
     is the initial all-zero state.  The fused kernel keeps the state on chip, so inside a run of
     consecutive iterations the boundaries are recorded (input, weights, starting state) and the state
     is recomputed on demand -- the value the reference stored -- when a later call resumes there
-    (e.g. forward() followed by forward(target_iter=k)).  Such a recomputed state is a constant: a
-    gradient does not flow back into the call that produced it (in the reference it would reach that
-    call's graph, which a completed backward has already freed).
+    (e.g. forward() followed by forward(target_iter=k)).  The record holds its own copy of the
+    channel input and of the previous posterior (UCN), so a caller that refills its xa buffer in place
+    between the calls still resumes from the state the reference stored (Boosted…py:512); a starting
+    state modified in place is detected (tensor version) and raises.  Such a recomputed state is a
+    constant: a gradient does not flow back into the call that produced it (in the reference it would
+    reach that call's graph, which a completed backward has already freed).  The final boundary of a
+    call, self.llr[last + 1], is that call's own output state and stays attached to its graph, as the
+    reference's self.llr[t + 1] does: resuming from it after a completed backward fails the same way
+    in both ("backward through the graph a second time").
   * gradients flow through the message state between the segments of one call (list-valued xa: one
     segment per iteration; split iteration lists), as through the reference's self.llr[t + 1].
 """
@@ -111,6 +117,9 @@ class BoostedNeuralLDPCDecoder(nn.Module):
             rec, off = st.rec, st.off
             with torch.no_grad():
                 state_in = rec["state_in"]
+                if state_in is not None and state_in._version != rec["state_ver"]:
+                    raise RuntimeError(f"self.llr[{k}] cannot be recomputed: the state its run started from was "
+                                       "modified in place after the call that recorded it")
                 w = lambda a: None if a is None else a[:off]  # noqa: E731
                 cfg = rec["cfg"]
                 _, st = decode_autograd(self.conn_mat.graph, cfg, rec["x"], off, w_cn=w(rec["w_cn"]),
@@ -354,8 +363,13 @@ class BoostedNeuralLDPCDecoder(nn.Module):
             self.llr[run[-1] + 1] = state
             if len(run) > 1:  # the boundaries inside the run: recomputed on demand (see the module docstring)
                 det = lambda a: None if a is None else a.detach()  # noqa: E731
-                rec = {"cfg": cfg, "x": x_in.detach(), "w_cn": det(wc), "w_ucn": det(wu), "w_vn": det(w_vn_all),
-                       "state_in": None if state_in is None else state_in.detach(), "app_prev": app_prev}
+                # the input and previous posterior are copied (the caller may refill them in place: a
+                # 1/T-size copy beside the T outputs); the starting state is module-owned, its version
+                # is checked when the record is used
+                rec = {"cfg": cfg, "x": x_in.detach().clone(), "w_cn": det(wc), "w_ucn": det(wu),
+                       "w_vn": det(w_vn_all), "state_in": det(state_in),
+                       "state_ver": None if state_in is None else state_in._version,
+                       "app_prev": None if app_prev is None else app_prev.clone()}
                 for off in range(1, len(run)):
                     self.llr[run[0] + off] = BoostedNeuralLDPCDecoder._Pending(rec, off)
             if has_vn and not listed:

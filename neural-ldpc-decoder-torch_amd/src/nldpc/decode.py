@@ -98,12 +98,13 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
 
 
 def decode_count(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn=None, w_ucn=None, bias=None,
-                 w_vn=None, y=None, convention: int = 0) -> torch.Tensor:
+                 w_vn=None, y=None, convention: int = 0, app_prev=None) -> torch.Tensor:
     """Count-only decode: int64 [T, 2] device tensor of (bit errors, frame errors) of
     every iteration's posterior -- what decode(...) followed by channel.ber_counts(outputs, y,
     convention=...) returns, counted inside the fused kernel (nldpc_forward_count) so the T posteriors
     are never written.  Configurations the fused path does not cover (UCN, a resumed state, a graph
-    without a compiled kernel) run decode + the device counter instead (both on the device)."""
+    without a compiled kernel, UCN resumed at first_iter > 0) run decode + the device counter instead
+    (both on the device); app_prev: the posterior of iteration first_iter - 1 for those UCN calls."""
     _require_device_tensor(xa, "xa")
     if xa.dim() != 3 or xa.shape[1] != graph.N or xa.shape[2] != graph.Z:
         raise ValueError(f"xa must be [B, {graph.N}, {graph.Z}], got {tuple(xa.shape)}")
@@ -116,9 +117,9 @@ def decode_count(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *
     fast = ctypes.c_int32(0)
     _lib.check(L.nldpc_fast_path(h, ctypes.byref(c), B, T, 0, ctypes.byref(fast)), "nldpc_fast_path")
     yb = None if y is None else (y != 0).to(torch.uint8).reshape(B, graph.N * graph.Z).contiguous()
-    if not fast.value:
+    if not fast.value or (cfg.ucn and cfg.first_iter > 0):  # (nldpc_forward_count has no app_prev)
         from .channel import ber_counts
-        outs, _, _ = decode(graph, cfg, xa, T, w_cn=w_cn, w_ucn=w_ucn, bias=bias, w_vn=w_vn)
+        outs, _, _ = decode(graph, cfg, xa, T, w_cn=w_cn, w_ucn=w_ucn, bias=bias, w_vn=w_vn, app_prev=app_prev)
         return ber_counts(list(outs), yb, convention=convention)
     counts = torch.zeros((T, 2), dtype=torch.int64, device=dev)
     xa_c = _f32c(xa)

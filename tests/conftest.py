@@ -17,6 +17,16 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+# GPU tests that start rank processes go first: they must be started by a process that has not touched
+# the GPU yet (test_distributed.py), whatever order the other test files would run in
+_FIRST = ("test_bench_launches_ranks_and_sums_counts", "test_two_rank_sharded_decode_on_gpu")
+
+
+def pytest_collection_modifyitems(config, items):
+    first = [it for it in items if it.name in _FIRST]
+    items[:] = sorted(first, key=lambda it: _FIRST.index(it.name)) + [it for it in items if it.name not in _FIRST]
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

@@ -149,14 +149,42 @@ def _gpu_worker(rank, world, port, total, T, q):
         raise
 
 
+def _bench_line(*args):
+    """One bench.py run as a child process (the parent never touches the GPU): its JSON line."""
+    import json
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+           "--no-sweep", "--no-count-only", "--no-profile", *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, f"bench.py {' '.join(args)} exited {r.returncode}:\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_bench_launches_ranks_and_sums_counts():
+    """bench.py's own multi-rank path on the one-GPU box: --gpus 2 starts the two rank processes itself
+    (launch_ranks -> torch.distributed.run), each decodes its shard of the global batch (b_offset), the
+    error counters are summed and the time is the max over ranks; only the transport is gloo instead of
+    RCCL (--backend gloo: both ranks on cuda:0).  The summed counts equal one rank decoding 2B."""
+    B = 48
+    two = _bench_line("--gpus", "2", "--backend", "gloo", "--batch", str(B))
+    one = _bench_line("--gpus", "1", "--batch", str(2 * B))
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["global_batch"] == 2 * B and two["config"]["per_gpu_batch"] == B
+    assert two["config"]["parallelism"] == "dp2" and two["scaling"] == "weak"
+    assert two["ber"]["bit_errors_last_iter"] == one["ber"]["bit_errors_last_iter"] > 0
+    assert two["ber"]["ber_per_iter"] == one["ber"]["ber_per_iter"]
+    assert two["ber"]["fer_last_iter"] == one["ber"]["fer_last_iter"]
+
+
 @pytest.mark.gpu
 def test_two_rank_sharded_decode_on_gpu():
     """Two rank processes decode the two shards of a BG2 z=384 batch with the product (HIP kernels,
     on-device channel at the rank's b_offset) and all-reduce the counters: the result equals one
     process decoding the whole batch.  Started before this process touches the GPU (a process that
     has initialised the GPU must not start others)."""
-    if torch.cuda.is_initialized():
-        pytest.skip("this process already initialised the GPU; rank processes must come from a clean parent")
+    # conftest.py runs the multi-process GPU tests before any other GPU test, so this holds by construction
+    assert not torch.cuda.is_initialized(), "rank processes must be started before this process touches the GPU"
     total, T, world = 9, 6, 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

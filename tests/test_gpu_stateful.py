@@ -70,3 +70,39 @@ def test_stateful_sequence_matches_reference(golden, name):
         elif p.grad is not None:
             assert not p.grad.any(), pname
     assert n > 0
+
+
+@pytest.mark.parametrize("dtype,nw", [(2, (3, 0, 3)), (1, (1, 1, 2))])
+def test_resume_after_caller_refills_input(dtype, nw):
+    """forward(x); x.copy_(next batch) in place; forward(x2, target_iter=[k..T-1]) resumes from the state
+    the first call reached at k -- computed from the ORIGINAL x, as the reference stores it
+    (BoostedNeuralLDPCDecoder.py:512) -- not from the refilled buffer."""
+    import boosted_neural_ldpc_decoder as bd
+    from boosted_neural_ldpc_decoder.BoostedNeuralLDPCDecoder import BoostedNeuralLDPCDecoder
+    from boosted_neural_ldpc_decoder.struct.DecoderType import DecoderType
+    from boosted_neural_ldpc_decoder.struct.NodeWeightSharingConfig import NodeWeightSharingConfig as NW
+    T, B, Z, k = 8, 3, 16, 5
+    conn = bd.ConnectingMatrixTorch(bd.ConnectingMatrix(Z, BG2), device=DEV)
+
+    def model():
+        m = BoostedNeuralLDPCDecoder(T, B, conn, node_weight_sharing_config=NW(*nw), decoding_type=DecoderType(dtype),
+                                     decoder_qms_qbit=5).to(DEV)
+        g = torch.Generator().manual_seed(7)
+        with torch.no_grad():
+            for _, p in m.named_parameters():
+                p.copy_(0.6 + 0.8 * torch.rand(p.shape, generator=g))
+        return m
+
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(B, 52, Z, generator=g) * 4 + 1).to(DEV)
+    x2 = (torch.randn(B, 52, Z, generator=g) * 4 + 1).to(DEV)
+    ref_model, dut = model(), model()
+    with torch.no_grad():
+        ref_model(x.clone())
+        ref = [o.clone() for o in ref_model(x2, target_iter=list(range(k, T)))]
+        buf = x.clone()
+        dut(buf)
+        buf.copy_(x2)  # the caller refills its input buffer in place
+        got = dut(x2, target_iter=list(range(k, T)))
+    for t, (a, b) in enumerate(zip(got, ref)):
+        assert torch.equal(a, b), f"iteration {k + t}: {(a != b).sum().item()} values differ"

@@ -15,7 +15,10 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define R16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
 template <int OP>
-__device__ __forceinline__ void body(float (&a)[16], f2 (&p)[16], float b0, float b1, f2 q0, f2 q1) {
+__device__ __forceinline__ void body(float (&a)[16], f2 (&p)[16], uint32_t (&u)[16], float b0, float b1, f2 q0, f2 q1) {
+    uint64_t ms[8];
+    uint64_t mk;
+    asm volatile("s_mov_b64 %0, 0x55" : "=s"(mk));
     // 16 groups x 16 independent instructions = 256 per trip
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
@@ -49,7 +52,141 @@ __device__ __forceinline__ void body(float (&a)[16], f2 (&p)[16], float b0, floa
 #define PK4(i) p[(i) & 3] = p[(i) & 3] + p[((i) & 7) | 8];
             R16(PK4)
         }
-        asm volatile("" : "+v"(a[0]), "+v"(p[0]));  // keep the groups from folding across trips
+        if constexpr (OP == 11) {  // v_med3_f32 with three VGPR sources
+#define MED3V(i) a[i] = __builtin_amdgcn_fmed3f(a[i], a[((i) + 5) & 15], a[((i) + 9) & 15]);
+            R16(MED3V)
+        }
+        if constexpr (OP == 12) {  // v_fma_f32 with three VGPR sources
+#define FMAV(i) a[i] = __builtin_fmaf(a[i], a[((i) + 5) & 15], a[((i) + 9) & 15]);
+            R16(FMAV)
+        }
+        if constexpr (OP == 13) {  // v_mul_f32 VGPR x SGPR (the check node's weight product)
+#define MULS(i) a[i] = a[i] * bb;
+            R16(MULS)
+        }
+        if constexpr (OP == 14) {  // v_cmp (VGPR vs VGPR -> SGPR pair) + v_cndmask: 8 pairs
+#define CSEL(i) if ((i) & 1) { a[i] = (a[(i) ^ 1] < a[((i) + 6) & 15]) ? a[i] : a[((i) + 3) & 15]; }
+            R16(CSEL)
+        }
+        if constexpr (OP == 15) {  // v_max_f32 with |x| modifiers on two VGPR sources
+#define MAXA(i) a[i] = __builtin_fmaxf(__builtin_fabsf(a[i]), __builtin_fabsf(a[((i) + 7) & 15]));
+            R16(MAXA)
+        }
+        if constexpr (OP == 16) {  // v_min_f32_e64 |x|, |y| (inline asm, VOP3 with abs modifiers)
+#define MINAA(i) asm("v_min_f32_e64 %0, |%0|, |%1|" : "+v"(a[i]) : "v"(a[((i) + 7) & 15]));
+            R16(MINAA)
+        }
+        if constexpr (OP == 17) {  // v_cndmask_b32_e64 with a fixed SGPR-pair mask
+#define CNDS(i) asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(a[((i) + 7) & 15]), "s"(mk));
+            R16(CNDS)
+        }
+        if constexpr (OP == 18) {  // v_cmp_lt_f32_e64 into 8 rotating SGPR pairs (results xor-ed once per group)
+#define CMPS(i) asm volatile("v_cmp_lt_f32_e64 %0, %1, %2" : "=s"(ms[(i) & 7]) : "v"(a[i]), "v"(a[((i) + 7) & 15]));
+            R16(CMPS)
+            a[0] = (ms[0] ^ ms[3] ^ ms[5]) & 1 ? a[0] : a[1];
+        }
+        if constexpr (OP == 19) {  // v_max_f32_e32 0, x (the ReLU)
+#define MAX0(i) asm("v_max_f32_e32 %0, 0, %0" : "+v"(a[i]));
+            R16(MAX0)
+        }
+        if constexpr (OP == 20) {  // v_min3_f32 with three VGPR sources
+#define MIN3V(i) asm("v_min3_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(a[((i) + 5) & 15]), "v"(a[((i) + 9) & 15]));
+            R16(MIN3V)
+        }
+        if constexpr (OP == 21) {  // v_med3_f32 with an |x| modifier and two VGPR sources + constant
+#define MED3K(i) asm("v_med3_f32 %0, %0, 0, |%1|" : "+v"(a[i]) : "v"(a[((i) + 5) & 15]));
+            R16(MED3K)
+        }
+        if constexpr (OP == 22) {  // v_cmp_eq_f32_e64 |x|, y into 8 rotating SGPR pairs
+#define CMPE(i) asm volatile("v_cmp_eq_f32_e64 %0, |%1|, %2" : "=s"(ms[(i) & 7]) : "v"(a[i]), "v"(a[((i) + 7) & 15]));
+            R16(CMPE)
+            a[0] = (ms[0] ^ ms[3] ^ ms[5]) & 1 ? a[0] : a[1];
+        }
+        if constexpr (OP == 23) {  // v_add_f32_e32, two VGPR sources, asm (compare with the C form)
+#define ADDV(i) asm("v_add_f32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(a[((i) + 7) & 15]));
+            R16(ADDV)
+        }
+        if constexpr (OP == 24) {
+#define X24(i) asm("v_add_u32_e32 %0, %0, %1" : "+v"(u[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X24)
+        }
+        if constexpr (OP == 25) {
+#define X25(i) asm("v_xor_b32_e32 %0, %0, %1" : "+v"(u[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X25)
+        }
+        if constexpr (OP == 26) {
+#define X26(i) asm("v_and_b32_e32 %0, %0, %1" : "+v"(u[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X26)
+        }
+        if constexpr (OP == 27) {
+#define X27(i) asm("v_bfi_b32 %0, %1, %0, %2" : "+v"(u[i]) : "v"(u[((i) + 3) & 15]), "v"(u[((i) + 7) & 15]));
+            R16(X27)
+        }
+        if constexpr (OP == 28) {
+#define X28(i) asm("v_lshlrev_b32_e32 %0, 1, %0" : "+v"(u[i]));
+            R16(X28)
+        }
+        if constexpr (OP == 29) {
+#define X29(i) asm("v_med3_u32 %0, %0, %1, %2" : "+v"(u[i]) : "v"(u[((i) + 3) & 15]), "v"(u[((i) + 7) & 15]));
+            R16(X29)
+        }
+        if constexpr (OP == 30) {
+#define X30(i) asm("v_min_u32_e32 %0, %0, %1" : "+v"(u[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X30)
+        }
+        if constexpr (OP == 31) {
+#define X31(i) asm("v_mov_b32_e32 %0, %1" : "=v"(u[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X31)
+        }
+        if constexpr (OP == 32) {
+#define X32(i) asm("v_sub_u32_e32 %0, %0, %1" : "+v"(u[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X32)
+        }
+        if constexpr (OP == 33) {
+#define X33(i) asm("v_add_f32_e64 %0, %0, |%1|" : "+v"(a[i]) : "v"(a[((i) + 7) & 15]));
+            R16(X33)
+        }
+        if constexpr (OP == 34) {
+#define X34(i) asm("v_fmac_f32_e32 %0, %1, %2" : "+v"(a[i]) : "v"(a[((i) + 7) & 15]), "v"(a[((i) + 3) & 15]));
+            R16(X34)
+        }
+        if constexpr (OP == 35) {
+#define X35(i) asm("v_add3_u32 %0, %0, %1, %2" : "+v"(u[i]) : "v"(u[((i) + 3) & 15]), "v"(u[((i) + 7) & 15]));
+            R16(X35)
+        }
+        if constexpr (OP == 36) {
+#define X36(i) asm("v_and_or_b32 %0, %0, %1, %2" : "+v"(u[i]) : "v"(u[((i) + 3) & 15]), "v"(u[((i) + 7) & 15]));
+            R16(X36)
+        }
+        if constexpr (OP == 37) {
+#define X37(i) asm("v_lshl_add_u32 %0, %0, 1, %1" : "+v"(u[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X37)
+        }
+        if constexpr (OP == 38) {
+#define X38(i) asm("v_cvt_f32_u32_e32 %0, %1" : "=v"(a[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X38)
+        }
+        if constexpr (OP == 39) {
+#define X39(i) asm("v_mul_f32_e64 %0, %0, -%1" : "+v"(a[i]) : "v"(a[((i) + 7) & 15]));
+            R16(X39)
+        }
+        if constexpr (OP == 40) {
+#define X40(i) asm("v_sub_f32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(a[((i) + 7) & 15]));
+            R16(X40)
+        }
+        if constexpr (OP == 41) {
+#define X41(i) asm("v_ldexp_f32 %0, %0, %1" : "+v"(a[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X41)
+        }
+        if constexpr (OP == 42) {
+#define X42(i) asm("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(u[i]) : "v"(u[((i) + 7) & 15]));
+            R16(X42)
+        }
+        if constexpr (OP == 43) {
+#define X43(i) asm("v_perm_b32 %0, %0, %1, %2" : "+v"(u[i]) : "v"(u[((i) + 3) & 15]), "v"(u[((i) + 7) & 15]));
+            R16(X43)
+        }
+        asm volatile("" : "+v"(a[0]), "+v"(p[0]), "+v"(u[0]));  // keep the groups from folding across trips
     }
 }
 
@@ -66,12 +203,15 @@ __global__ __launch_bounds__(TPB) void kern(float* out, unsigned long long* cyc,
     const f2 q0 = {b0, b1}, q1 = {b1, b0};
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    for (int r = 0; r < R; ++r) body<OP>(a, p, b0, b1, q0, q1);
+    uint32_t u[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) u[i] = __float_as_uint(a[i]) * 2654435761u;
+    for (int r = 0; r < R; ++r) body<OP>(a, p, u, b0, b1, q0, q1);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * (TPB / 64) + threadIdx.x / 64] = t1 - t0;
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s += a[i] + p[i].x + p[i].y;
+    for (int i = 0; i < 16; ++i) s += a[i] + p[i].x + p[i].y + (float)(u[i] & 1023);
     out[blockIdx.x * TPB + threadIdx.x] = s;
 }
 
@@ -101,17 +241,16 @@ void run(const char* name, float* d, unsigned long long* dc) {
 
 template <int OP>
 void sweep(const char* name, float* d, unsigned long long* dc) {
-    run<OP, 256>(name, d, dc);
-    run<OP, 512>(name, d, dc);
     run<OP, 1024>(name, d, dc);
     run<OP, 1024, 2>(name, d, dc);
 }
 
-int main() {
+int main(int argc, char**) {
     float* d;
     unsigned long long* dc;
     (void)hipMalloc(&d, 512 * 1024 * 4);
     (void)hipMalloc(&dc, 512 * 16 * 8);
+    if (argc < 2) {  // (r3 first pass; "valu_rate2 2" runs the second set only)
     sweep<0>("v_add_f32 (16 indep)", d, dc);
     sweep<1>("v_fma_f32 (16 indep)", d, dc);
     sweep<7>("v_min_f32 (16 indep)", d, dc);
@@ -123,5 +262,41 @@ int main() {
     sweep<9>("v_add_f32 (2 interleaved chains)", d, dc);
     sweep<6>("v_pk_add_f32 (1 dependent chain)", d, dc);
     sweep<10>("v_pk_add_f32 (4 interleaved chains)", d, dc);
+    sweep<11>("v_med3_f32 (3 VGPR sources)", d, dc);
+    sweep<12>("v_fma_f32 (3 VGPR sources)", d, dc);
+    sweep<13>("v_mul_f32 (VGPR x SGPR)", d, dc);
+    sweep<14>("v_cmp + v_cndmask (per pair: 2 instr)", d, dc);
+    }
+    if (argc == 3) {
+    sweep<24>("v_add_u32_e32", d, dc);
+    sweep<25>("v_xor_b32_e32", d, dc);
+    sweep<26>("v_and_b32_e32", d, dc);
+    sweep<27>("v_bfi_b32", d, dc);
+    sweep<28>("v_lshlrev_b32_e32", d, dc);
+    sweep<29>("v_med3_u32", d, dc);
+    sweep<30>("v_min_u32_e32", d, dc);
+    sweep<31>("v_mov_b32_e32", d, dc);
+    sweep<32>("v_sub_u32_e32", d, dc);
+    sweep<33>("v_add_f32_e64 |x|", d, dc);
+    sweep<34>("v_fmac_f32_e32", d, dc);
+    sweep<35>("v_add3_u32", d, dc);
+    sweep<36>("v_and_or_b32", d, dc);
+    sweep<37>("v_lshl_add_u32", d, dc);
+    sweep<38>("v_cvt_f32_u32", d, dc);
+    sweep<39>("v_mul_f32_e64 -x", d, dc);
+    sweep<40>("v_sub_f32_e32", d, dc);
+    sweep<41>("v_ldexp_f32", d, dc);
+    sweep<42>("v_mul_u32_u24", d, dc);
+    sweep<43>("v_perm_b32", d, dc);
+    return 0;
+    }
+    sweep<16>("v_min_f32_e64 |x|,|y| (asm)", d, dc);
+    sweep<17>("v_cndmask_b32_e64 (SGPR mask)", d, dc);
+    sweep<18>("v_cmp_lt_f32_e64 -> SGPR", d, dc);
+    sweep<19>("v_max_f32_e32 0, x", d, dc);
+    sweep<20>("v_min3_f32 (3 VGPR)", d, dc);
+    sweep<21>("v_med3_f32 x, 0, |y|", d, dc);
+    sweep<22>("v_cmp_eq_f32_e64 |x|, y -> SGPR", d, dc);
+    sweep<23>("v_add_f32_e32 (asm, 2 VGPR)", d, dc);
     return 0;
 }
