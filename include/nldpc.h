@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NLDPC_ABI_VERSION 2
+#define NLDPC_ABI_VERSION 3
 
 enum nldpc_status {
     NLDPC_OK = 0,
@@ -81,6 +81,18 @@ int nldpc_graph_destroy(nldpc_graph* g);
 int nldpc_graph_dims(const nldpc_graph* g, int32_t* dims);
 /* host copies of the C-order edge tables: check, variable, shift (mod Z) of every edge */
 int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t* shift);
+/* (ABI 3) A register-resident kernel compiled at run time for this lifted graph (gen_fused.py --jit
+ *      output, `hipcc --genco` for gfx950; entry point nldpc_fx, or nldpc_fxb for the backward): the
+ *      library's own fused kernels cover a fixed set of (base graph, Z); any other graph gets its kernels
+ *      this way, per mode (0 decode, 1 decode + save for backward, 2 / 3 count-only, 4 backward) and
+ *      kind, with the geometry they were generated for (codewords per workgroup, threads, waves per
+ *      part).  The graph keeps the loaded module until nldpc_graph_destroy.  No-op for a graph the
+ *      library already covers.  Replaces nothing in the reference (its dense path has no per-Z code);
+ *      it is what makes ConnectingMatrix(Z, basegraph) at any Z (ConnectingMatrix.py:5-53) fast. */
+int nldpc_graph_attach_kernel(nldpc_graph* g, int32_t mode, int32_t kind, const void* code, size_t bytes,
+                              int32_t G, int32_t threads, int32_t waves_per_part);
+/* (ABI 3) *mask: bit (mode * 4 + kind) set when that fused kernel exists for the graph (modes as above) */
+int nldpc_graph_kernels(const nldpc_graph* g, uint32_t* mask);
 
 /* ---- execution path.  *eligible = 1 when nldpc_forward with these arguments runs the fused
  *      register-resident kernel: a (base graph, lifting size) compiled in, no incoming message state
@@ -90,6 +102,8 @@ int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t*
  *      NLDPC_FLAG_NO_STATE.  Otherwise the streaming kernels run and need both buffers. */
 int nldpc_fast_path(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, int32_t saving,
                     int32_t* eligible);
+/*      (ABI 3) saving = 2 / 3 asks the same for nldpc_forward_count (all-zero codeword, decoder convention /
+ *      any convention or codeword), whose fused kernels are separate variants. */
 
 /* ---- decode forward: replaces NeuralLDPCDecoder.forward (NeuralLDPCDecoder.py:44-100) and
  *      BoostedNeuralLDPCDecoder.forward (BoostedNeuralLDPCDecoder.py:260-538).

@@ -110,10 +110,11 @@ MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel
 
 
 def auto_geometry(hb, Z):
-    """(G, P, Q) for a lifted graph: G codewords x P parts x Z/Q lanes per workgroup, whole waves, at
-    most 1024 threads, at most MAX_STATE_REGS state floats per thread, check rows that fit LDS.
-    Prefers >= 512 threads, then fewer LDS chunks (fewer barriers), then more threads, then fewer
-    copies per thread."""
+    """(G, P, Q) for a lifted graph: G codewords x P parts x Z/Q lanes per workgroup, at most 1024
+    threads, at most MAX_STATE_REGS state floats per thread, check rows that fit LDS.  A part's lanes are
+    padded to whole waves (the extra lanes repeat live ones, Spec.lanes_pad), at most a third of them
+    idle.  Prefers >= 512 threads, then fewer LDS chunks (fewer barriers), then fewer idle lanes, then
+    more threads, then fewer copies per thread."""
     rows, cols = np.nonzero(hb != -1)
     deg = np.bincount(cols, minlength=hb.shape[1])
     multi = [int(d) for d in deg if d > 1]
@@ -123,10 +124,11 @@ def auto_geometry(hb, Z):
         ZT = Z // Q
         for G in (1, 2, 4, 8, 16, 32):
             lanes = G * ZT
-            if lanes % 64:
+            pad = -(-lanes // 64) * 64
+            if pad * 3 > lanes * 4:  # more than a quarter of the part idle
                 continue
             for P in (8, 7, 6, 5, 4, 3, 2, 1):
-                threads = P * lanes
+                threads = P * pad
                 if threads > 1024:
                     continue
                 load = [0] * P
@@ -142,7 +144,7 @@ def auto_geometry(hb, Z):
                     if acc + d > cap:
                         nchunks, acc = nchunks + 1, 0
                     acc += int(d)
-                key = (threads >= 512, -nchunks, threads, -Q)
+                key = (threads >= 512, -nchunks, -(pad - lanes) / pad, threads, -Q)
                 if best is None or key > best[0]:
                     best = (key, (G, P, Q))
     if best is None:
@@ -239,9 +241,13 @@ class Spec:
         else:
             self.cn_units = [[[(i, q) for i in sorted(rows, key=lambda i: -len(self.row_edges[i])) for q in range(Q)]
                               for rows in self.cn_rows[ci]] for ci in range(len(self.chunks))]
-        self.lanes = G * self.ZT  # threads per part
-        self.threads = P * self.lanes
-        assert self.threads <= 1024 and self.lanes % 64 == 0, (tag, self.threads)
+        self.lanes = G * self.ZT  # live threads per part
+        # a part occupies whole waves: lanes past the live ones repeat live lanes (same codeword and copies,
+        # so they write the same values to the same places) and contribute nothing to counts and sums
+        self.lanes_pad = -(-self.lanes // 64) * 64
+        self.padded = self.lanes_pad != self.lanes
+        self.threads = P * self.lanes_pad
+        assert self.threads <= 1024, (tag, self.threads)
         self.max_dc = max(len(r) for r in self.row_edges)
         self.hb_cols = cols  # column of each C-order edge
 
@@ -254,7 +260,7 @@ def emit(S: Spec) -> str:
     # wrapped lane copies by scalar lane masks (own_lv): needs waves of 64 consecutive copies of one codeword
     WRAPM = WRAPMASK and G == 1 and ZT % 64 == 0
     w(f"// ---- {S.tag}: M={S.M} N={S.N} E={S.E} Z={Z}; workgroup = {G} codeword(s) x {S.P} part(s) x {ZT} lanes "
-      f"= {S.threads} threads, {Q} cop{'y' if Q == 1 else 'ies'} per lane; register slots/part "
+      f"= {S.threads} threads{' (padded parts)' if S.padded else ''}, {Q} cop{'y' if Q == 1 else 'ies'} per lane; register slots/part "
       f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B")
     w(f"namespace fused_{S.tag} {{")
     w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E};")
@@ -747,7 +753,7 @@ def emit(S: Spec) -> str:
     # allocator insert phi copies and spill).  The parts still meet at every s_barrier: a hardware
     # barrier counts waves, not program counters, and every part executes the same barrier sequence.
     # this thread's codeword counters (recomputed at each flush: no register held across the iteration)
-    cnt_slot = "cntl" if G == 1 else f"cntl + (int)((threadIdx.x % {S.lanes}) / {ZT}) * 32"
+    cnt_slot = "cntl"  # the kernel passes this codeword's counters
     cnt_flush = "flush_wave" if G == 1 else "flush"  # one codeword per wave: reduce the wave first
     for p in range(S.P):
         if PARTS and p not in PARTS:
@@ -756,7 +762,7 @@ def emit(S: Spec) -> str:
         nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
         w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
-          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw) {{")
+          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw, bool dup_) {{")
         for i in range(NP(p)):
             w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
         for i in range(NS(p)):
@@ -847,7 +853,7 @@ def emit(S: Spec) -> str:
         if "vn" not in SKIP:
             w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
-        w(f"        if constexpr (CNT) {{ if (it >= 1) ps.{cnt_flush}({cnt_slot}, it - 1); else ps.ec = 0; }}")
+        w(f"        if constexpr (CNT) {{ if (dup_) ps.ec = 0; if (it >= 1) ps.{cnt_flush}({cnt_slot}, it - 1); else ps.ec = 0; }}")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
         w(f"        const rsrc_t nr = make_rsrc(pn ? pn + blk * {NZ} : a.xa, pn ? nlive * {4 * NZ} : 0);")
         w("        const uint8_t* nmp = (SAVE && a.symask) ? a.symask + it * a.symask_stride : nullptr;")
@@ -944,7 +950,7 @@ def emit(S: Spec) -> str:
         w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
         w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr);")
-        w(f"    if constexpr (CNT) ps.{cnt_flush}({cnt_slot}, a.T - 1);")
+        w(f"    if constexpr (CNT) {{ if (dup_) ps.ec = 0; ps.{cnt_flush}({cnt_slot}, a.T - 1); }}")
         w("    if (a.c2v_out) {")
         for q in range(Q):
             for k, e in enumerate(S.slots[p]):
@@ -952,12 +958,18 @@ def emit(S: Spec) -> str:
         w("    }")
         w("}")
     w("template <int KIND, int MODE>")
-    w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void kernel(FusedArgs a) {{")
+    w("__device__ __forceinline__ void kernel_body(const FusedArgs& a) {")
     w(f"    __shared__ float lds_all[{CF * G * S.nbuf}];")
     w("    const int t = threadIdx.x;")
-    w(f"    // every wave lies in one part ({S.lanes} threads per part): the part is wave-uniform")
-    w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes});")
-    w(f"    const int r = t - p * {S.lanes};")
+    w(f"    // every wave lies in one part ({S.lanes_pad} threads per part): the part is wave-uniform")
+    w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes_pad});")
+    if S.padded:  # lanes past the live ones repeat live lanes (Spec.lanes_pad)
+        w(f"    const int r0_ = t - p * {S.lanes_pad};")
+        w(f"    const bool dup_ = r0_ >= {S.lanes};")
+        w(f"    const int r = dup_ ? r0_ - {S.lanes} : r0_;")
+    else:
+        w(f"    const int r = t - p * {S.lanes};")
+        w("    const bool dup_ = false;")
     w(f"    const int g = r / {ZT};")
     w(f"    const int u = r - g * {ZT};")
     w(f"    const int64_t blk = (int64_t)blockIdx.x * {G};  // first codeword of the workgroup")
@@ -974,11 +986,16 @@ def emit(S: Spec) -> str:
     w(f"    __shared__ uint32_t app_all[{G * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
     w(f"    uint32_t* appw = app_all + g * {S.N * S.WZX};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
-    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all, app_all, appw)", indent="    ")
+    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_)",
+              indent="    ")
     w("    if constexpr (CNT) {")
     w("        __syncthreads();")
     w("        if (t < a.T) count_iteration(a, cnt_all, nlive, t);")
     w("    }")
+    w("}")
+    w("template <int KIND, int MODE>")
+    w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void kernel(FusedArgs a) {{")
+    w("    kernel_body<KIND, MODE>(a);")
     w("}")
     w("#undef D1_BYPASS")
     w("#undef UCNW")
@@ -1001,7 +1018,7 @@ def emit_bwd(S: Spec) -> str:
     * mask_{k-1} + sum of the column's other dL/dv2c_k (prefix + suffix, as vnb_kernel), and the
     cumulative VN-weight chain (carry per channel value).  Weight gradients: per-wave partial sums."""
     Z, G, Q, ZT, NZ, E, N = S.Z, S.G, S.Q, S.ZT, S.N * S.Z, S.E, S.N
-    WP = S.lanes // 64  # waves per part
+    WP = S.lanes_pad // 64  # waves per part
     L = []
     w = L.append
     CF = S.chunk_floats
@@ -1041,8 +1058,8 @@ def emit_bwd(S: Spec) -> str:
         w(f"{indent}  ctb_ += du_ * xp_;")
         w(f"{indent}  bstore(cyr, vo, {X(j, q)}, du_ * wvn[{j}]); }}")
 
-    def col_partial(j, indent):
-        w(f"{indent}if (a.p_vn) {{ const float s_ = wave_sum(ctb_); if (lane0) a.p_vn[pv + {j}] = s_; }}")
+    def col_partial(j, indent):  # (lanes repeating a live one add nothing: Spec.lanes_pad)
+        w(f"{indent}if (a.p_vn) {{ const float s_ = wave_sum(dup_ ? 0.f : ctb_); if (lane0) a.p_vn[pv + {j}] = s_; }}")
 
     # ---------------------------------------------------------------- LDS write / read-back
     for p in range(S.P):
@@ -1063,7 +1080,7 @@ def emit_bwd(S: Spec) -> str:
             w("template <int KIND>")
             w(f"__device__ __forceinline__ void rdb_p{p}_c{ci}({state_params(p)}, const float* lds, "
               f"int u, const FusedBwdArgs& a, int it, uint32_t vo, rsrc_t xr, rsrc_t sxp, rsrc_t cyr, cfloat_p wvn, "
-              f"int64_t pv, bool lane0) {{")
+              f"int64_t pv, bool lane0, bool dup_) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
             for q in range(Q):
                 for k, e in mine:
@@ -1088,7 +1105,7 @@ def emit_bwd(S: Spec) -> str:
         w("template <int KIND>")
         w(f"__device__ __forceinline__ void vnb_p{p}({state_params(p)}, const FusedBwdArgs& a, "
           f"int it, uint32_t vo, uint32_t vm, rsrc_t gr, rsrc_t mr, rsrc_t xr, rsrc_t sxp, rsrc_t cyr, cfloat_p wvn, "
-          f"int64_t pv, bool lane0) {{")
+          f"int64_t pv, bool lane0, bool dup_) {{")
         w("    const bool chain_on = KIND != NLDPC_NEURAL && a.w_vn;")
         w("    const QRange qr = q_range(a.qbit);")
         s0 = 0
@@ -1141,7 +1158,7 @@ def emit_bwd(S: Spec) -> str:
     w(f"static __constant__ int32_t e_shift[{E}] = {{{', '.join(str(int(x)) for x in S.shift)}}};")
     w("template <int KIND, int DC>")
     w("__device__ __forceinline__ void cnb_rows(float* lds, int u, const FusedBwdArgs& a, int it, int t0, int n, "
-      "int e0c, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0) {")
+      "int e0c, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_) {")
     w("    asm volatile(\"\" : \"+v\"(u));")
     w("    for (int r = 0; r < n; ++r) {")
     w("        const int e0 = cn_tab[t0 + r];")
@@ -1201,11 +1218,11 @@ def emit_bwd(S: Spec) -> str:
     w("        }")
     w("        if (a.p_cn) {")
     w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) { const float s_ = wave_sum(gwa[k]); if (lane0) a.p_cn[pc + e0 + k] = s_; }")
+    w("            for (int k = 0; k < DC; ++k) { const float s_ = wave_sum(dup_ ? 0.f : gwa[k]); if (lane0) a.p_cn[pc + e0 + k] = s_; }")
     w("        }")
     w("        if (KIND == NLDPC_NEURAL && a.p_bias) {")
     w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) { const float s_ = wave_sum(gba[k]); if (lane0) a.p_bias[pc + e0 + k] = s_; }")
+    w("            for (int k = 0; k < DC; ++k) { const float s_ = wave_sum(dup_ ? 0.f : gba[k]); if (lane0) a.p_bias[pc + e0 + k] = s_; }")
     w("        }")
     w("    }")
     w("}")
@@ -1215,7 +1232,7 @@ def emit_bwd(S: Spec) -> str:
         sp = max(len(S.slots[p]), 1)
         w("template <int KIND>")
         w(f"__device__ __forceinline__ void bwd_p{p}(const FusedBwdArgs& a, float* lds, int u, int64_t blk, int nlive, "
-          f"uint32_t vo, uint32_t vm, uint32_t vcw, int slot, bool lane0) {{")
+          f"uint32_t vo, uint32_t vm, uint32_t vcw, int slot, bool lane0, bool dup_) {{")
         for q in range(Q):
             w(f"    float g{q}[{sp}];")
         w(f"    const rsrc_t cyr = make_rsrc(a.carry ? a.carry + blk * {NZ} : nullptr, a.carry ? nlive * {4 * NZ} : 0);")
@@ -1256,24 +1273,26 @@ def emit_bwd(S: Spec) -> str:
             w(f"        wrb_p{p}_c{ci}<KIND>({state_args()}, lds, u, gr, mr, vo, vm);")
             w("        __syncthreads();")
             for dc, t0, n in groups[(p, ci)]:
-                w(f"        cnb_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]}, svr, vcw, pc, lane0);")
+                w(f"        cnb_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]}, svr, vcw, pc, lane0, dup_);")
             w("        __syncthreads();")
-            w(f"        rdb_p{p}_c{ci}<KIND>({state_args()}, lds, u, a, it, vo, xr, sxp, cyr, wvn, pv, lane0);")
+            w(f"        rdb_p{p}_c{ci}<KIND>({state_args()}, lds, u, a, it, vo, xr, sxp, cyr, wvn, pv, lane0, dup_);")
             w("        __syncthreads();")
         w("        const float* gq_ = it >= 1 ? a.gy.p[it - 1] : nullptr;  // dL/dy_{k-1}")
         w("        const uint8_t* mq_ = (a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t gr1 = {rs('gq_', 4, NZ)};")
         w(f"        const rsrc_t mr1 = {rs('mq_', 1, NZ)};")
-        w(f"        vnb_p{p}<KIND>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0);")
+        w(f"        vnb_p{p}<KIND>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0, dup_);")
         w("    }")
         w("}")
 
     w("template <int KIND>")
-    w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void bwd_kernel(FusedBwdArgs a) {{")
+    w("__device__ __forceinline__ void bwd_body(const FusedBwdArgs& a) {")
     w(f"    __shared__ float lds_all[{CF * G}];")
     w("    const int t = threadIdx.x;")
-    w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes});")
-    w(f"    const int r = t - p * {S.lanes};")
+    w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes_pad});")
+    w(f"    const int r0_ = t - p * {S.lanes_pad};")
+    w(f"    const bool dup_ = r0_ >= {S.lanes};  // a lane repeating a live one (Spec.lanes_pad)")
+    w(f"    const int r = dup_ ? r0_ - {S.lanes} : r0_;")
     w(f"    const int g = r / {ZT};")
     w(f"    const int u = r - g * {ZT};")
     w(f"    const int64_t blk = (int64_t)blockIdx.x * {G};")
@@ -1281,11 +1300,15 @@ def emit_bwd(S: Spec) -> str:
     w(f"    const uint32_t vo = g < nlive ? 4u * (g * {NZ} + u) : 0x80000000u;")
     w("    const uint32_t vm = vo >> 2;")
     w(f"    const uint32_t vcw = g < nlive ? 4u * (g * {E * Z}) : 0x80000000u;  // codeword base in [E][Z] (CN gathers)")
-    w("    const int slot = blockIdx.x * WP + __builtin_amdgcn_readfirstlane(r >> 6);")
+    w("    const int slot = blockIdx.x * WP + __builtin_amdgcn_readfirstlane(r0_ >> 6);")
     w("    const bool lane0 = (t & 63) == 0;")
     w(f"    float* lds = lds_all + g * {CF};")
     for p in range(S.P):
-        w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0);")
+        w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0, dup_);")
+    w("}")
+    w("template <int KIND>")
+    w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void bwd_kernel(FusedBwdArgs a) {{")
+    w("    bwd_body<KIND>(a);")
     w("}")
     w("}  // namespace")
     return "\n".join(L)
@@ -1294,9 +1317,37 @@ def emit_bwd(S: Spec) -> str:
 MODES = (0, 1, 2, 3)  # forward kernels: decode / decode + save for backward / count-only (all-zero, LLR > 0) / count-only (general)
 
 
+def jit_source(hb, Z, kind, mode):
+    """One register-resident kernel for any lifted graph, compiled at run time (nldpc/jit.py: hipcc
+    --genco, nldpc_graph_attach_kernel): the (graph, Z) -> geometry choice of auto_geometry, the same
+    emitted code as the library's own kernels, one (kind, mode) instantiation behind an unmangled entry
+    point -- nldpc_fx (MODE 0-3) or nldpc_fxb (mode 4, the backward).  Returns (source, geometry dict)."""
+    hb = np.asarray(hb, dtype=np.int64)
+    G, P, Q = auto_geometry(hb, Z)
+    S = Spec("jit", hb, Z, G, P, Q, pipe=PIPE and mode in (0, 2, 3))  # the SAVE kernels keep one buffer
+    L = ["// GENERATED by gen_fused.py jit_source -- do not edit.", "#include <hip/hip_runtime.h>",
+         '#include "nldpc_fused.h"', "namespace nldpc {", emit(S) if mode < 4 else emit_bwd(S), "}  // namespace nldpc"]
+    lb = f"__launch_bounds__({S.threads}, {(S.threads + 255) // 256})"
+    if mode < 4:
+        L.append(f'extern "C" __global__ {lb} void nldpc_fx(nldpc::FusedArgs a) {{ '
+                 f"nldpc::fused_jit::kernel_body<{kind}, {mode}>(a); }}")
+    else:
+        L.append(f'extern "C" __global__ {lb} void nldpc_fxb(nldpc::FusedBwdArgs a) {{ '
+                 f"nldpc::fusedb_jit::bwd_body<{kind}>(a); }}")
+    return "\n".join(L) + "\n", {"G": G, "threads": S.threads, "waves_per_part": S.lanes_pad // 64,
+                                 "P": P, "Q": Q, "padded": S.padded}
+
+
 def main():
     """Writes OUTDIR/fused_<tag>_s<MODE>.hip (one translation unit per base graph and MODE variant,
     so make -j compiles them in parallel) and OUTDIR/fused_table.hip (the FusedSpec table)."""
+    if sys.argv[1] == "--jit":  # --jit BASEGRAPH.txt Z KIND MODE OUT.hip: one run-time kernel's source
+        hb = np.loadtxt(sys.argv[2], int, delimiter="\t")
+        src, geo = jit_source(hb, int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]))
+        with open(sys.argv[6], "w") as f:
+            f.write(src)
+        print(geo)
+        return
     if sys.argv[1] == "--list":  # file names, for the Makefile
         print(" ".join([f"fused_{t[0]}_s{v}.hip" for t in SPECS for v in MODES] +
                        [f"fused_{t[0]}_bwd.hip" for t in SPECS] + ["fused_table.hip"]))
@@ -1363,7 +1414,7 @@ def main():
         ks = ", ".join("{" + ", ".join(f"fused_{S.tag}_kernel_s{v}({k})" for k in range(4)) + "}" for v in MODES)
         kb = ", ".join(f"fused_{S.tag}_bwd({k})" for k in range(4))
         src.append(f"        {{\"{S.tag}\", {S.M}, {S.N}, {S.Z}, {S.E}, {S.G}, {S.threads}, basegraph_{S.tag}, "
-                   f"{{{ks}}}, {{{kb}}}, {S.lanes // 64}}},")
+                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}}},")
     src.append("    };")
     src.append(f"    *n = {len(specs)};")
     src.append("    return tab;")

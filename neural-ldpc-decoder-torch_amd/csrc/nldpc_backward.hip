@@ -382,7 +382,7 @@ static hipError_t reduce_launch(float* part, int64_t rows, int64_t nb, int64_t w
 // ---- fused backward (register-resident kernels generated by gen_fused.py emit_bwd) ---------------
 static bool fused_bwd_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T, bool state_grads) {
     static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
-    if (disabled || state_grads || (cfg->flags & NLDPC_FLAG_STREAM) || g->fused < 0) return false;
+    if (disabled || state_grads || (cfg->flags & NLDPC_FLAG_STREAM) || !fused_launch(g, 4, cfg->kind)) return false;
     if (cfg->kind == NLDPC_QMS && !qms_active(cfg->qbit)) return false;  // QMS saved state = int8 codes
     return !cfg->ucn && cfg->vn_prefix == 0 && T <= kFusedMaxT;
 }
@@ -393,8 +393,7 @@ struct FusedWork {
 };
 
 static FusedWork fused_work_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T) {
-    int n = 0;
-    const FusedSpec& f = fused_specs(&n)[g->fused];
+    const FusedLaunch f = fused_launch(g, 4, cfg->kind);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     FusedWork w;
     w.nslots = (B + f.G - 1) / f.G * f.waves_per_part;
@@ -411,8 +410,7 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
                           const float* w_cn, const float* bias, const float* w_vn, const float* const* grad_outs,
                           const void* saved, float* g_w_cn, float* g_bias, float* g_w_vn, void* work,
                           hipStream_t s) {
-    int n = 0;
-    const FusedSpec& f = fused_specs(&n)[g->fused];
+    const FusedLaunch f = fused_launch(g, 4, cfg->kind);
     const FusedWork W = fused_work_layout(g, cfg, B, T);
     const SavedLayout SL = saved_layout(g, cfg, B, T);
     const DevGraph& G = g->dev;
@@ -445,7 +443,7 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
     void* args[] = {&a};
     const int64_t blocks = (B + f.G - 1) / f.G;
     prof_start(PROF_FUSED_BWD, s);
-    hipError_t e = hipLaunchKernel(f.bwd[cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args, 0, s);
+    hipError_t e = f.launch(blocks, args, s);
     prof_stop(s);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "fused backward launch");

@@ -269,20 +269,23 @@ SavedLayout saved_layout(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     return L;
 }
 
-static bool fused_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T, bool saving) {
+// mode: 0 decode, 1 decode + save for backward, 2 / 3 count-only (the fused kernel variants)
+static bool fused_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T, int mode) {
+    const bool saving = mode == 1;
     static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
     if (disabled || (cfg->flags & NLDPC_FLAG_STREAM)) return false;
     // the SAVE kernels write what the backward needs (QMS: int8 codes, which need an active quantiser)
     if (saving && cfg->kind == NLDPC_QMS && !qms_active(cfg->qbit)) return false;
-    return g->fused >= 0 && !cfg->c2v_in && T <= kFusedMaxT;
+    return fused_launch(g, mode, cfg->kind) && !cfg->c2v_in && T <= kFusedMaxT;
 }
 
 static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, const float* xa,
                          const float* w_cn, const float* w_ucn, const float* bias, const float* w_vn,
                          float* const* outs, const float* app_prev, float* c2v, void* saved, hipStream_t s,
                          const uint8_t* cnt_y = nullptr, int32_t cnt_conv = 0, int64_t* counts = nullptr) {
-    int n = 0;
-    const FusedSpec& f = fused_specs(&n)[g->fused];
+    const int mode = saved ? 1 : (counts ? ((cnt_y || cnt_conv) ? 3 : 2) : 0);
+    const FusedLaunch f = fused_launch(g, mode, cfg->kind);
+    if (!f) return fail(NLDPC_EUNSUPPORTED, "no register-resident kernel for this graph / mode / kind");
     FusedArgs fa{};
     fa.B = B;
     fa.T = T;
@@ -323,8 +326,7 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     void* args[] = {&fa};
     const int64_t blocks = (B + f.G - 1) / f.G;
     prof_start(PROF_FUSED, s);
-    const int mode = saved ? 1 : (counts ? ((cnt_y || cnt_conv) ? 3 : 2) : 0);
-    hipError_t e = hipLaunchKernel(f.kernels[mode][cfg->kind], dim3((unsigned)blocks), dim3(f.threads), args, 0, s);
+    hipError_t e = f.launch(blocks, args, s);
     prof_stop(s);
     if (e == hipSuccess) e = hipGetLastError();
     if (stamp_file && e == hipSuccess) {
@@ -351,7 +353,8 @@ extern "C" int nldpc_fast_path(const nldpc_graph* g, const nldpc_cfg* cfg, int64
     int st = validate_cfg(g, cfg, B, T);
     if (st) return st;
     if (!eligible) return fail(NLDPC_EINVAL, "nldpc_fast_path: null output");
-    *eligible = fused_eligible(g, cfg, T, saving != 0) ? 1 : 0;
+    if (saving < 0 || saving > 3) return fail(NLDPC_EINVAL, "nldpc_fast_path: saving is 0, 1 (or 2 / 3: count-only)");
+    *eligible = fused_eligible(g, cfg, T, saving) ? 1 : 0;
     return NLDPC_OK;
 }
 
@@ -385,7 +388,7 @@ extern "C" int nldpc_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t
     }
     DeviceGuard guard(g->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const bool fused = fused_eligible(g, cfg, T, saved != nullptr);
+    const bool fused = fused_eligible(g, cfg, T, saved != nullptr ? 1 : 0);
     if ((cfg->flags & NLDPC_FLAG_FUSED) && !fused)
         return fail(NLDPC_EUNSUPPORTED, "nldpc_forward: the fused path is not available for this call");
     if (fused) {
@@ -468,7 +471,7 @@ extern "C" int nldpc_forward_count(const nldpc_graph* g, const nldpc_cfg* cfg, i
     if (cfg->kind == NLDPC_NEURAL && (!w_cn || !bias))
         return fail(NLDPC_EINVAL, "nldpc_forward_count: the Neural decoder needs w_cn and bias");
     if (cfg->vn_cumulative && !w_vn) return fail(NLDPC_EINVAL, "nldpc_forward_count: vn_cumulative needs w_vn");
-    if (!fused_eligible(g, cfg, T, false) || (cfg->ucn && cfg->first_iter > 0))
+    if (!fused_eligible(g, cfg, T, (y || convention) ? 3 : 2) || (cfg->ucn && cfg->first_iter > 0))
         return fail(NLDPC_EUNSUPPORTED, "nldpc_forward_count: needs the fused path (a compiled base graph, no UCN, "
                                         "fresh state, T <= 64); use nldpc_forward + nldpc_ber_count instead");
     DeviceGuard guard(g->device);

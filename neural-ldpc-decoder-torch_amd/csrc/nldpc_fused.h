@@ -765,4 +765,19 @@ struct FusedSpec {
 
 const FusedSpec* fused_specs(int* n);
 
+// How to launch the register-resident kernel of (graph, MODE, kind) (MODE 4: the backward): one compiled
+// into the library (fused_specs table, hipLaunchKernel) or one compiled at run time for this graph and
+// attached (nldpc_graph_attach_kernel, hipModuleLaunchKernel); empty when neither exists.
+struct FusedLaunch {
+    const void* host = nullptr;
+    hipFunction_t fn = nullptr;
+    int32_t G = 0, threads = 0, waves_per_part = 0;
+    explicit operator bool() const { return host != nullptr || fn != nullptr; }
+    hipError_t launch(int64_t blocks, void** args, hipStream_t s) const {
+        if (fn) return hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, (unsigned)threads, 1, 1, 0, s, args, nullptr);
+        return hipLaunchKernel(host, dim3((unsigned)blocks), dim3((unsigned)threads), args, 0, s);
+    }
+};
+FusedLaunch fused_launch(const nldpc_graph* g, int mode, int kind);
+
 }  // namespace nldpc

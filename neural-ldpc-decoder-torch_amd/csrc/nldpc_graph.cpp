@@ -246,11 +246,76 @@ extern "C" int nldpc_graph_create(int32_t M, int32_t N, int32_t Z, const int32_t
     }
 }
 
+namespace nldpc {
+FusedLaunch fused_launch(const nldpc_graph* g, int mode, int kind) {
+    FusedLaunch L;
+    if (!g || mode < 0 || mode > 4 || kind < 0 || kind > 3) return L;
+    if (g->fused >= 0) {
+        int n = 0;
+        const FusedSpec& f = fused_specs(&n)[g->fused];
+        L.host = mode == 4 ? f.bwd[kind] : f.kernels[mode][kind];
+        L.G = f.G;
+        L.threads = f.threads;
+        L.waves_per_part = f.waves_per_part;
+    } else if (g->jit_fn[mode][kind]) {
+        L.fn = g->jit_fn[mode][kind];
+        L.G = g->jit_G;
+        L.threads = g->jit_threads;
+        L.waves_per_part = g->jit_wpp;
+    }
+    return L;
+}
+}  // namespace nldpc
+
+extern "C" int nldpc_graph_attach_kernel(nldpc_graph* g, int32_t mode, int32_t kind, const void* code, size_t bytes,
+                                         int32_t G, int32_t threads, int32_t waves_per_part) {
+    if (!g || !code || !bytes) return fail(NLDPC_EINVAL, "nldpc_graph_attach_kernel: null argument");
+    if (mode < 0 || mode > 4 || kind < NLDPC_SP || kind > NLDPC_NEURAL)
+        return fail(NLDPC_EINVAL, "nldpc_graph_attach_kernel: mode is 0-4 and kind an nldpc kind");
+    if (G <= 0 || threads <= 0 || threads > 1024 || threads % 64 || waves_per_part <= 0)
+        return fail(NLDPC_EINVAL, "nldpc_graph_attach_kernel: bad geometry");
+    if (g->fused >= 0) return NLDPC_OK;  // the library's own kernels serve this graph
+    bool first = true;
+    for (int m = 0; m < 5; ++m)
+        for (int k = 0; k < 4; ++k) first = first && !g->jit_fn[m][k];
+    if (!first && (G != g->jit_G || threads != g->jit_threads || waves_per_part != g->jit_wpp))
+        return fail(NLDPC_EINVAL, "nldpc_graph_attach_kernel: geometry differs from the graph's attached kernels");
+    if (g->jit_fn[mode][kind]) return NLDPC_OK;
+    DeviceGuard guard(g->device);
+    hipModule_t mod = nullptr;
+    NLDPC_HIP_CHECK(hipModuleLoadData(&mod, code));
+    hipFunction_t fn = nullptr;
+    hipError_t e = hipModuleGetFunction(&fn, mod, mode == 4 ? "nldpc_fxb" : "nldpc_fx");
+    if (e != hipSuccess) {
+        (void)hipModuleUnload(mod);
+        return hip_fail(e, "hipModuleGetFunction(nldpc_fx)");
+    }
+    g->jit_mod[mode][kind] = mod;
+    g->jit_fn[mode][kind] = fn;
+    g->jit_G = G;
+    g->jit_threads = threads;
+    g->jit_wpp = waves_per_part;
+    return NLDPC_OK;
+}
+
+extern "C" int nldpc_graph_kernels(const nldpc_graph* g, uint32_t* mask) {
+    if (!g || !mask) return fail(NLDPC_EINVAL, "nldpc_graph_kernels: null pointer");
+    uint32_t m = 0;
+    for (int mode = 0; mode < 5; ++mode)
+        for (int k = 0; k < 4; ++k)
+            if (fused_launch(g, mode, k)) m |= 1u << (mode * 4 + k);
+    *mask = m;
+    return NLDPC_OK;
+}
+
 extern "C" int nldpc_graph_destroy(nldpc_graph* g) {
     if (!g) return NLDPC_OK;
     {
         DeviceGuard guard(g->device);
         if (g->blob) (void)hipFree(g->blob);
+        for (auto& row : g->jit_mod)
+            for (hipModule_t m : row)
+                if (m) (void)hipModuleUnload(m);
     }
     delete[] g->h_chk;
     delete[] g->h_var;

@@ -45,6 +45,11 @@ struct nldpc_graph {
     nldpc::DevGraph dev;
     int32_t device;
     int32_t fused;  // index into nldpc::fused_specs() of a compiled register-resident kernel, or -1
+    // register-resident kernels compiled at run time for this graph and attached by
+    // nldpc_graph_attach_kernel: [MODE 0-3 | 4 = backward][kind], one code object each
+    hipModule_t jit_mod[5][4];
+    hipFunction_t jit_fn[5][4];
+    int32_t jit_G, jit_threads, jit_wpp;  // their geometry (one per graph)
     void* blob;  // device allocation backing the tables
     // host mirrors
     int32_t* h_chk;

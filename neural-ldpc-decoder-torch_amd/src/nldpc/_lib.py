@@ -20,13 +20,13 @@ LIB_PATH = os.environ.get("NLDPC_LIB_PATH") or os.path.normpath(os.path.join(_HE
 
 NLDPC_OK, NLDPC_EINVAL, NLDPC_EHIP, NLDPC_EUNSUPPORTED = 0, 1, 2, 3
 NLDPC_SP, NLDPC_MS, NLDPC_QMS, NLDPC_NEURAL = 0, 1, 2, 3
-ABI_VERSION = 2
+ABI_VERSION = 3
 FLAG_STREAM, FLAG_FUSED, FLAG_NO_STATE = 1, 2, 4
 
 # every symbol include/nldpc.h declares
 EXPORTED = (
     "nldpc_abi_version", "nldpc_last_error", "nldpc_graph_create", "nldpc_graph_destroy", "nldpc_graph_dims",
-    "nldpc_graph_edges", "nldpc_fast_path", "nldpc_saved_bytes", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
+    "nldpc_graph_edges", "nldpc_graph_attach_kernel", "nldpc_graph_kernels", "nldpc_fast_path", "nldpc_saved_bytes", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
     "nldpc_awgn_llr", "nldpc_profile_begin", "nldpc_profile_end", "nldpc_bce_workspace", "nldpc_bce_loss",
     "nldpc_bce_grad", "nldpc_forward_count", "nldpc_channel_llr", "nldpc_hbm_probe",
 )
@@ -72,6 +72,8 @@ def _declare(lib):
         "nldpc_graph_destroy": (_i32, [_vp]),
         "nldpc_graph_dims": (_i32, [_vp, ctypes.POINTER(_i32)]),
         "nldpc_graph_edges": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+        "nldpc_graph_attach_kernel": (_i32, [_vp, _i32, _i32, _vp, ctypes.c_size_t, _i32, _i32, _i32]),
+        "nldpc_graph_kernels": (_i32, [_vp, ctypes.POINTER(ctypes.c_uint32)]),
         "nldpc_fast_path": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _i32, ctypes.POINTER(_i32)]),
         "nldpc_saved_bytes": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, ctypes.POINTER(ctypes.c_size_t)]),
         "nldpc_forward": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _vp, _vp, _vp, _vp, _vp, _PP, _vp, _vp,

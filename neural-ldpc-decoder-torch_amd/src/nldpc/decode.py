@@ -12,7 +12,7 @@ from dataclasses import dataclass
 
 import torch
 
-from . import _lib
+from . import _lib, jit
 from .graph import LiftedGraph
 
 KIND_SP, KIND_MS, KIND_QMS, KIND_NEURAL = _lib.NLDPC_SP, _lib.NLDPC_MS, _lib.NLDPC_QMS, _lib.NLDPC_NEURAL
@@ -70,6 +70,8 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
     c = cfg.c_struct(c2v_in)
     L = _lib.lib()
     h = graph.handle(dev)
+    if cfg.path != "stream" and not c2v_in and T <= 64:  # a graph the library has no kernel for: compile one
+        jit.ensure(graph, dev, cfg.kind, 1 if save else 0)
     fast = ctypes.c_int32(0)
     _lib.check(L.nldpc_fast_path(h, ctypes.byref(c), B, T, int(bool(save)), ctypes.byref(fast)), "nldpc_fast_path")
     if c2v_in:
@@ -114,9 +116,12 @@ def decode_count(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *
     c.flags |= _lib.FLAG_NO_STATE
     L = _lib.lib()
     h = graph.handle(dev)
-    fast = ctypes.c_int32(0)
-    _lib.check(L.nldpc_fast_path(h, ctypes.byref(c), B, T, 0, ctypes.byref(fast)), "nldpc_fast_path")
     yb = None if y is None else (y != 0).to(torch.uint8).reshape(B, graph.N * graph.Z).contiguous()
+    mode = 3 if (yb is not None or convention) else 2  # the count-only kernel variant
+    if cfg.path != "stream" and T <= 64 and not (cfg.ucn and cfg.first_iter > 0):
+        jit.ensure(graph, dev, cfg.kind, mode)
+    fast = ctypes.c_int32(0)
+    _lib.check(L.nldpc_fast_path(h, ctypes.byref(c), B, T, mode, ctypes.byref(fast)), "nldpc_fast_path")
     if not fast.value or (cfg.ucn and cfg.first_iter > 0):  # (nldpc_forward_count has no app_prev)
         from .channel import ber_counts
         outs, _, _ = decode(graph, cfg, xa, T, w_cn=w_cn, w_ucn=w_ucn, bias=bias, w_vn=w_vn, app_prev=app_prev)
@@ -150,6 +155,10 @@ def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, 
     c = cfg.c_struct(c2v_in)
     L = _lib.lib()
     h = graph.handle(dev)
+    qms_identity = cfg.kind == KIND_QMS and cfg.qbit not in (6, 5, -5, 4, 3)
+    if (cfg.path != "stream" and not cfg.ucn and cfg.vn_prefix == 0 and T <= 64 and not qms_identity
+            and grad_state is None and not want_state_grad and not c2v_in):  # the fused backward's conditions
+        jit.ensure(graph, dev, cfg.kind, 4)
     nbytes = ctypes.c_size_t(0)
     _lib.check(L.nldpc_backward_workspace(h, ctypes.byref(c), B, T, ctypes.byref(nbytes)), "nldpc_backward_workspace")
     work = torch.empty((max(int(nbytes.value), 1),), dtype=torch.uint8, device=dev)

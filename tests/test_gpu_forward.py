@@ -168,10 +168,15 @@ def test_fast_path_selection():
     from nldpc import _lib
     from nldpc.decode import KIND_NEURAL, DecodeCfg
     L = _lib.lib()
-    for bg, Z, want in ((BG2, 384, 1), (BG2, 16, 1), (WIMAX, 24, 1), (BG2, 96, 1), (BG2, 64, 0), (BG2, 104, 0)):
+    from nldpc import jit
+    # built in: BG2 z=384/16/96, WiMAX z=24; any other lifting size gets its kernels compiled at run time
+    # (nldpc.jit: z=64 and z=104 -- 104 = 8 x 13 needs parts padded to whole waves)
+    for bg, Z, want in ((BG2, 384, 1), (BG2, 16, 1), (WIMAX, 24, 1), (BG2, 96, 1), (BG2, 64, 1), (BG2, 104, 1)):
         g = _graph(bg, Z)
         for save, ucn, exp in ((0, False, want), (1, False, want), (0, True, want)):
-            cfg = DecodeCfg(KIND_NEURAL if not ucn else 1, ucn=ucn).c_struct(False)
+            kind = KIND_NEURAL if not ucn else 1
+            jit.ensure(g, DEV, kind, save)  # (a no-op for the built-in ones)
+            cfg = DecodeCfg(kind, ucn=ucn).c_struct(False)
             out = ctypes.c_int32(-1)
             _lib.check(L.nldpc_fast_path(g.handle(DEV), ctypes.byref(cfg), 4, 20, save, ctypes.byref(out)))
             assert out.value == exp, (Z, save, ucn)
@@ -401,3 +406,67 @@ def test_tanh_table_vs_this_hosts_torch():
         with open(log, "a") as f:
             f.write(f"tanh table vs this host's torch.tanh: {msg}\n")
     assert int(ulps.max()) <= 1, msg
+
+
+@pytest.mark.parametrize("Z", [52, 104, 208])
+@pytest.mark.parametrize("kind", [3, 1, 2])
+def test_runtime_kernel_lifting_sizes_match_oracle(Z, kind):
+    """5G NR BG2 lifting sizes with no built-in kernel (52 = 4 x 13 and 104 = 8 x 13: parts padded to
+    whole waves; 208: 4 parts of 256 lanes) on the register-resident path (path="fused" is required):
+    the kernel is generated and compiled at run time (nldpc.jit, cached), and its outputs equal the CPU
+    oracle's bit for bit (Neural, Boosted MS / QMS with per-check CN and cumulative VN weights).  The
+    count-only variant counts what the outputs hold."""
+    from nldpc.channel import ber_counts
+    from nldpc.decode import DecodeCfg, decode, decode_count
+    from oracle.ldpc_oracle import OracleGraph, boosted_forward, neural_forward, quantize
+    T, B = 5, 3
+    g = _graph(BG2, Z)
+    og = OracleGraph(BG2, Z)
+    gen = torch.Generator().manual_seed(Z + kind)
+    x = (2 * (-1 + 0.85 * torch.randn(B, 52, Z, generator=gen)) / 0.7225).float()
+    if kind == 3:
+        w = torch.rand(T, g.E, generator=gen) * 1.2
+        b = torch.randn(T, g.E, generator=gen) * 0.1
+        kw = dict(w_cn=w.to(DEV), bias=b.to(DEV))
+        cfg = DecodeCfg(kind, path="fused")
+        ref = torch.stack(neural_forward(og, x, list(w), list(b))).numpy()
+    else:
+        if kind == 2:
+            x = quantize(x, 5)
+        wc = 0.5 + torch.rand(T, 42, generator=gen)
+        wv = 0.8 + 0.4 * torch.rand(T, 52, generator=gen)
+        kw = dict(w_cn=wc[:, torch.as_tensor(g.chk)].contiguous().to(DEV), w_vn=wv.to(DEV))
+        cfg = DecodeCfg(kind, qbit=5, vn_cumulative=True, path="fused")
+        r = boosted_forward(og, x, dtype=kind, q=5, nw=(2, 0, 2), iters=list(range(T)), w_cn=lambda t: wc[t],
+                            w_ucn=lambda t: None, w_vn=lambda t: wv[t])
+        ref = torch.stack([r[t] for t in range(T)]).numpy()
+    outs, _, _ = decode(g, cfg, x.to(DEV), T, **kw)
+    got = outs.cpu().numpy()
+    assert np.array_equal(got, ref.reshape(got.shape)), f"{(got != ref.reshape(got.shape)).sum()} values differ"
+    counts = decode_count(g, cfg, x.to(DEV), T, **kw)
+    assert torch.equal(counts, ber_counts(list(outs)))
+
+
+def test_runtime_kernel_training_step_matches_streaming():
+    """The run-time compiled saving forward (mode 1) and backward (mode 4) at a lifting size with padded
+    parts (BG2 z=104, QMS q=5, per-edge CN and per-column VN weights): the same outputs and weight
+    gradients as the streaming kernels."""
+    from nldpc.decode import DecodeCfg, decode, decode_backward
+    T, B, Z = 6, 4, 104
+    g = _graph(BG2, Z)
+    gen = torch.Generator().manual_seed(104)
+    from oracle.ldpc_oracle import quantize
+    x = quantize((2 * (-1 + 0.85 * torch.randn(B, 52, Z, generator=gen)) / 0.7225).float(), 5).to(DEV)
+    wc = (0.5 + torch.rand(T, g.E, generator=gen)).to(DEV)
+    wv = (0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV)
+    gy = [torch.randn(B, 52 * Z, generator=gen).to(DEV) for _ in range(T)]
+    res = {}
+    for path in ("stream", "fused"):
+        cfg = DecodeCfg(2, qbit=5, vn_cumulative=True, path=path)
+        outs, _, saved = decode(g, cfg, x, T, w_cn=wc, w_vn=wv, save=True)
+        grads = decode_backward(g, cfg, x, T, gy, list(outs), saved, w_cn=wc, w_vn=wv)
+        res[path] = (outs, grads[0], grads[3])
+    assert torch.equal(res["stream"][0], res["fused"][0])
+    for k in (1, 2):
+        a, b = res["stream"][k].cpu().numpy(), res["fused"][k].cpu().numpy()
+        np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-5 * np.abs(a).max())

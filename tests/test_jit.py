@@ -1,0 +1,56 @@
+"""Run-time kernels for lifting sizes the library was not built for (nldpc.jit, csrc/gen_fused.py
+jit_source), on the CPU: every 5G NR base-graph-2 lifting size has a register-resident
+geometry and generates, and one kernel compiles into a gfx950 code object with the entry point the
+library attaches (the GPU tests run them: tests/test_gpu_forward.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+BG2 = np.loadtxt(os.path.join(ROOT, "resources", "basegraph2_set0.txt"), int, delimiter="\t")
+# TS 38.212 Table 5.3.2-1: the lifting sizes (every a x 2^j up to 384)
+NR_Z = sorted({a * 2 ** j for a in (2, 3, 5, 7, 9, 11, 13, 15) for j in range(8) if a * 2 ** j <= 384})
+
+
+def _gen():
+    from nldpc import jit
+    return jit._generator()
+
+
+def test_every_nr_lifting_size_has_a_geometry():
+    gen = _gen()
+    assert len(NR_Z) == 51
+    for Z in NR_Z:
+        G, P, Q = gen.auto_geometry(BG2, Z)
+        S = gen.Spec("t", BG2, Z, G, P, Q, pipe=True)
+        assert S.threads <= 1024 and S.lanes_pad % 64 == 0 and (S.lanes_pad - S.lanes) * 4 <= S.lanes_pad, Z
+        assert max(len(s) for s in S.slots) * Q <= gen.MAX_STATE_REGS, Z
+
+
+@pytest.mark.parametrize("Z", [2, 13, 52, 104, 208, 320])
+def test_jit_source_generates(Z):
+    gen = _gen()
+    for mode in (0, 4):
+        src, geo = gen.jit_source(BG2, Z, 3, mode)
+        entry = "nldpc_fxb" if mode == 4 else "nldpc_fx"
+        assert f'extern "C" __global__' in src and f"void {entry}(" in src
+        assert geo["threads"] <= 1024 and geo["threads"] % 64 == 0
+
+
+def test_jit_compiles_a_code_object(tmp_path, monkeypatch):
+    """hipcc --genco of one run-time kernel (BG2 z=52, Neural decode): the cached code object exists and
+    holds the unmangled entry point nldpc_graph_attach_kernel looks up."""
+    import shutil
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc not installed")
+    from nldpc import jit
+    monkeypatch.setenv("NLDPC_JIT_CACHE", str(tmp_path))
+    path, geo = jit.code_object(BG2, 52, 3, 0)
+    assert os.path.dirname(path) == str(tmp_path) and os.path.getsize(path) > 1000
+    assert geo["G"] == 2 and geo["padded"]
+    assert b"nldpc_fx" in open(path, "rb").read()
+    again, _ = jit.code_object(BG2, 52, 3, 0)  # a cache hit: same file, no recompile
+    assert again == path
+    shutil.rmtree(tmp_path, ignore_errors=True)
