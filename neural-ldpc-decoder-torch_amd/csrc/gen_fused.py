@@ -136,7 +136,8 @@ def auto_geometry(hb, Z):
                     load[int(np.argmin(load))] += d
                 if Q * max(load) > MAX_STATE_REGS:
                     continue
-                cap = ((LDS_BYTES - 4 * G * app_words(hb.shape[1], Z)) // (4 * G) - 32) // Z  # edges per LDS chunk
+                GL = G + (1 if pad != lanes else 0)  # (+1: the repeating lanes' LDS region, Spec.G_lds)
+                cap = ((LDS_BYTES - 4 * GL * app_words(hb.shape[1], Z)) // (4 * GL) - 32) // Z  # edges per LDS chunk
                 if cap < int(row_deg.max()):
                     continue
                 nchunks, acc = 1, 0
@@ -202,9 +203,21 @@ class Spec:
         # (used by the MS kernels only: in the QMS kernels the extra scalar state measured slower, 180 -> 217 ms
         # at cfg3 NW(1,1,2), register allocation; UCNW in the generated code)
         self.ucn_wave = self.ZT % 64 == 0 and Z % 32 == 0 and os.environ.get("NLDPC_GEN_UCNWAVE", "1") == "1"
-        cap = ((LDS_BYTES - 4 * G * app_words(self.N, Z)) // (4 * G) - 32) // Z
+        self.lanes = G * self.ZT  # live threads per part
+        # A part occupies whole waves.  The lanes past the live ones (padded parts) run the code of the
+        # first live lanes (same copies) on an LDS region of their own and with global offsets out of
+        # every descriptor's range: nothing they compute reaches the live codewords' messages, outputs,
+        # counters or gradient sums.  (Sharing the live lanes' LDS would race: a check node updates its
+        # slots in place, and a repeating lane in a later wave could read the updated value.)
+        self.lanes_pad = -(-self.lanes // 64) * 64
+        self.padded = self.lanes_pad != self.lanes
+        self.G_lds = G + (1 if self.padded else 0)  # codeword LDS regions (+1: the repeating lanes')
+        self.threads = P * self.lanes_pad
+        assert self.threads <= 1024, (tag, self.threads)
+        GL = self.G_lds
+        cap = ((LDS_BYTES - 4 * GL * app_words(self.N, Z)) // (4 * GL) - 32) // Z
         if pipe:  # two buffers; only the count-only counters (G*128 B) share the remaining KiB
-            cap = ((160 * 1024 - 1024 - 4 * G * app_words(self.N, Z)) // (8 * G) - (32 if G > 1 else 0)) // Z
+            cap = ((160 * 1024 - 1024 - 4 * GL * app_words(self.N, Z)) // (8 * GL) - (32 if GL > 1 else 0)) // Z
         self.chunks = []  # (row_begin, row_end, edge_begin, edge_end)
         r0 = 0
         while r0 < self.M:
@@ -217,7 +230,7 @@ class Spec:
             self.chunks.append((r0, r1, e0, self.row_edges[r1 - 1][-1] + 1))
             r0 = r1
         self.chunk_floats = max(e1 - e0 for _, _, e0, e1 in self.chunks) * Z
-        if G > 1:  # codeword stride = 1 (mod 32 banks) so lanes of different codewords do not collide
+        if GL > 1:  # codeword stride = 1 (mod 32 banks) so lanes of different codewords do not collide
             self.chunk_floats += (1 - self.chunk_floats) % 32
         self.nbuf = 2 if pipe else 1
         self.cn_rows = [balance(list(range(r0, r1)), lambda i: len(self.row_edges[i]), P)
@@ -241,13 +254,6 @@ class Spec:
         else:
             self.cn_units = [[[(i, q) for i in sorted(rows, key=lambda i: -len(self.row_edges[i])) for q in range(Q)]
                               for rows in self.cn_rows[ci]] for ci in range(len(self.chunks))]
-        self.lanes = G * self.ZT  # live threads per part
-        # a part occupies whole waves: lanes past the live ones repeat live lanes (same codeword and copies,
-        # so they write the same values to the same places) and contribute nothing to counts and sums
-        self.lanes_pad = -(-self.lanes // 64) * 64
-        self.padded = self.lanes_pad != self.lanes
-        self.threads = P * self.lanes_pad
-        assert self.threads <= 1024, (tag, self.threads)
         self.max_dc = max(len(r) for r in self.row_edges)
         self.hb_cols = cols  # column of each C-order edge
 
@@ -828,7 +834,7 @@ def emit(S: Spec) -> str:
         w("    uint32_t d1m = 0;  // UCN: hard decisions of this thread's degree-1 posteriors")
         w(f"    const rsrc_t apr = make_rsrc(a.app_prev ? a.app_prev + blk * {NZ} : a.xa, a.app_prev ? nlive * {4 * NZ} : 0);")
         w("    if (KIND != NLDPC_NEURAL && a.ucn) {")
-        w(f"        for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
+        w(f"        for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
         w("        __syncthreads();")
         w("    }")
         w("    for (int it = 0; it < a.T; ++it) {")
@@ -904,7 +910,7 @@ def emit(S: Spec) -> str:
               f"ps, d1m);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
                 w("        if (KIND != NLDPC_NEURAL && !UCNW && a.ucn) {")
-                w(f"            for (int i_ = threadIdx.x; i_ < {G * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
+                w(f"            for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
                 w("        }")
 
         K = len(S.chunks)
@@ -959,7 +965,7 @@ def emit(S: Spec) -> str:
         w("}")
     w("template <int KIND, int MODE>")
     w("__device__ __forceinline__ void kernel_body(const FusedArgs& a) {")
-    w(f"    __shared__ float lds_all[{CF * G * S.nbuf}];")
+    w(f"    __shared__ float lds_all[{CF * S.G_lds * S.nbuf}];")
     w("    const int t = threadIdx.x;")
     w(f"    // every wave lies in one part ({S.lanes_pad} threads per part): the part is wave-uniform")
     w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes_pad});")
@@ -976,15 +982,15 @@ def emit(S: Spec) -> str:
     w(f"    const int nlive = a.B - blk < {G} ? (int)(a.B - blk) : {G};")
     w("    // lane byte offsets into the block's codewords; a lane past the last codeword gets an offset")
     w("    // beyond every descriptor's range (its loads read 0, its stores are dropped)")
-    w(f"    const uint32_t vo = g < nlive ? 4u * (g * {NZ} + u) : 0x80000000u;  // [N][Z] layouts")
-    w(f"    const uint32_t vc = g < nlive ? 4u * (g * {S.E * Z} + u) : 0x80000000u;  // [E][Z] c2v state")
+    w(f"    const uint32_t vo = g < nlive && !dup_ ? 4u * (g * {NZ} + u) : 0x80000000u;  // [N][Z] layouts")
+    w(f"    const uint32_t vc = g < nlive && !dup_ ? 4u * (g * {S.E * Z} + u) : 0x80000000u;  // [E][Z] c2v state")
     w(f"    const rsrc_t xr = make_rsrc(a.xa + blk * {NZ}, nlive * {4 * NZ});")
     w(f"    const rsrc_t cr = make_rsrc(a.c2v_out ? a.c2v_out + blk * {S.E * Z} : a.xa, nlive * {4 * S.E * Z});")
-    w(f"    float* lds = lds_all + g * {CF * S.nbuf};")
+    w(f"    float* lds = lds_all + (dup_ ? {G} : g) * {CF * S.nbuf};  // (repeating lanes: their own region)")
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
     w(f"    __shared__ int cnt_all[{G * 32}];  // count-only decode: per codeword, two iterations per word")
-    w(f"    __shared__ uint32_t app_all[{G * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
-    w(f"    uint32_t* appw = app_all + g * {S.N * S.WZX};")
+    w(f"    __shared__ uint32_t app_all[{S.G_lds * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
+    w(f"    uint32_t* appw = app_all + (dup_ ? {G} : g) * {S.N * S.WZX};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
     each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_)",
               indent="    ")
@@ -1287,7 +1293,7 @@ def emit_bwd(S: Spec) -> str:
 
     w("template <int KIND>")
     w("__device__ __forceinline__ void bwd_body(const FusedBwdArgs& a) {")
-    w(f"    __shared__ float lds_all[{CF * G}];")
+    w(f"    __shared__ float lds_all[{CF * S.G_lds}];")
     w("    const int t = threadIdx.x;")
     w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes_pad});")
     w(f"    const int r0_ = t - p * {S.lanes_pad};")
@@ -1297,12 +1303,12 @@ def emit_bwd(S: Spec) -> str:
     w(f"    const int u = r - g * {ZT};")
     w(f"    const int64_t blk = (int64_t)blockIdx.x * {G};")
     w(f"    const int nlive = a.B - blk < {G} ? (int)(a.B - blk) : {G};")
-    w(f"    const uint32_t vo = g < nlive ? 4u * (g * {NZ} + u) : 0x80000000u;")
+    w(f"    const uint32_t vo = g < nlive && !dup_ ? 4u * (g * {NZ} + u) : 0x80000000u;")
     w("    const uint32_t vm = vo >> 2;")
-    w(f"    const uint32_t vcw = g < nlive ? 4u * (g * {E * Z}) : 0x80000000u;  // codeword base in [E][Z] (CN gathers)")
+    w(f"    const uint32_t vcw = g < nlive && !dup_ ? 4u * (g * {E * Z}) : 0x80000000u;  // codeword base in [E][Z] (CN gathers)")
     w("    const int slot = blockIdx.x * WP + __builtin_amdgcn_readfirstlane(r0_ >> 6);")
     w("    const bool lane0 = (t & 63) == 0;")
-    w(f"    float* lds = lds_all + g * {CF};")
+    w(f"    float* lds = lds_all + (dup_ ? {G} : g) * {CF};  // (repeating lanes: their own region)")
     for p in range(S.P):
         w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0, dup_);")
     w("}")

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void ber_kernel(const float* llr, const uint8_
 
 // ---------------------------------------------------------------- multi-iteration BCE loss
 constexpr int kBceMaxK = 64;
-constexpr int kBceBlocks = 512;  // element blocks per term
+constexpr int kBceBlocks = 2048;  // element blocks (workgroups) of the loss pass
 struct BceArgs {
     const float* x[kBceMaxK];
     float coef[kBceMaxK];
@@ -119,43 +119,42 @@ __device__ __forceinline__ float bce_term(float x, float t) {
     return (1.f - t) * x - ls;
 }
 
-// One workgroup per (element block x, term k): the fp64 sum of term k's BCE over its elements, 16 B
-// loads; the finish kernel combines sum_k coef_k * S_k / n in a fixed order (deterministic).
+// One workgroup per element block, every term: each thread reads its labels once and the K logits at
+// the same positions (16 B loads), and sums coef_k * term in fp64 (fp32 terms, as torch's); the finish
+// kernel adds the per-block partial sums in a fixed order (deterministic) and divides by n.  (r2 read
+// the labels once per term, twice the bytes at cfg5: 6.7 ms for 8.2 GB of logits.)
 __global__ __launch_bounds__(256) void bce_loss_kernel(BceArgs a, const float* __restrict__ target, int64_t n,
                                                        double* __restrict__ part) {
     __shared__ double red[4];
-    const int k = blockIdx.y;
-    const float* __restrict__ x = a.x[k];
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(target)) & 15) == 0;
+    bool vec = (reinterpret_cast<uintptr_t>(target) & 15) == 0;
+    for (int k = 0; k < a.K; ++k) vec = vec && (reinterpret_cast<uintptr_t>(a.x[k]) & 15) == 0;
     const int64_t n4 = vec ? n / 4 : 0;
     for (int64_t i = i0; i < n4; i += stride) {
-        const float4 v = reinterpret_cast<const float4*>(x)[i];
         const float4 t = target ? reinterpret_cast<const float4*>(target)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        acc += (double)bce_term(v.x, t.x) + (double)bce_term(v.y, t.y) + (double)bce_term(v.z, t.z) +
-               (double)bce_term(v.w, t.w);
+        for (int k = 0; k < a.K; ++k) {
+            const float4 v = reinterpret_cast<const float4*>(a.x[k])[i];
+            acc += (double)a.coef[k] * (((double)bce_term(v.x, t.x) + (double)bce_term(v.y, t.y)) +
+                                        ((double)bce_term(v.z, t.z) + (double)bce_term(v.w, t.w)));
+        }
     }
-    for (int64_t i = 4 * n4 + i0; i < n; i += stride) acc += (double)bce_term(x[i], target ? target[i] : 0.f);
+    for (int64_t i = 4 * n4 + i0; i < n; i += stride) {
+        const float t = target ? target[i] : 0.f;
+        for (int k = 0; k < a.K; ++k) acc += (double)a.coef[k] * (double)bce_term(a.x[k][i], t);
+    }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) part[(int64_t)k * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(64) void bce_finish_kernel(const double* __restrict__ part, int nb, BceArgs a, int64_t n,
+__global__ __launch_bounds__(64) void bce_finish_kernel(const double* __restrict__ part, int nb, int64_t n,
                                                         float* __restrict__ loss, int accumulate) {
-    __shared__ double tk[kBceMaxK];
-    for (int k = threadIdx.x; k < a.K; k += 64) {
-        double s = 0.0;
-        for (int b = 0; b < nb; ++b) s += part[(int64_t)k * nb + b];
-        tk[k] = s;
-    }
-    __syncthreads();
     if (threadIdx.x == 0) {
         double s = 0.0;
-        for (int k = 0; k < a.K; ++k) s += (double)a.coef[k] * tk[k];
+        for (int b = 0; b < nb; ++b) s += part[b];
         const float v = (float)(s / (double)n);
         *loss = accumulate ? *loss + v : v;
     }
@@ -226,19 +225,19 @@ extern "C" int nldpc_hbm_probe(int32_t kind, float* dst, const float* src, int64
 
 extern "C" int nldpc_bce_workspace(int64_t n, int32_t K, size_t* bytes) {
     if (!bytes || n <= 0 || K <= 0) return fail(NLDPC_EINVAL, "nldpc_bce_workspace: bad argument");
-    *bytes = (size_t)kBceMaxK * kBceBlocks * sizeof(double);
+    *bytes = (size_t)kBceBlocks * sizeof(double);
     return NLDPC_OK;
 }
 
-static int bce_blocks(int64_t n) {  // ~16 float4 per thread, at most kBceBlocks element blocks per term
-    const int64_t b = (n + 256 * 64 - 1) / (256 * 64);
+static int bce_blocks(int64_t n) {  // ~8 float4 of every term per thread, at most kBceBlocks element blocks
+    const int64_t b = (n + 256 * 32 - 1) / (256 * 32);
     return (int)(b < 1 ? 1 : (b < kBceBlocks ? b : kBceBlocks));
 }
 
 extern "C" int nldpc_bce_loss(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
                               float* loss, void* work, size_t work_bytes, void* stream) {
     if (!logits || !coef || !loss || !work || n <= 0 || K <= 0) return fail(NLDPC_EINVAL, "nldpc_bce_loss: bad argument");
-    if (work_bytes < (size_t)kBceMaxK * kBceBlocks * sizeof(double))
+    if (work_bytes < (size_t)kBceBlocks * sizeof(double))
         return fail(NLDPC_EINVAL, "nldpc_bce_loss: workspace too small");
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int nb = bce_blocks(n);
@@ -251,8 +250,8 @@ extern "C" int nldpc_bce_loss(const float* const* logits, int32_t K, const float
             a.coef[k] = coef[k0 + k];
         }
         double* part = static_cast<double*>(work);
-        hipLaunchKernelGGL(bce_loss_kernel, dim3(nb, a.K), dim3(256), 0, s, a, target, n, part);
-        hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(64), 0, s, part, nb, a, n, loss, k0 > 0 ? 1 : 0);
+        hipLaunchKernelGGL(bce_loss_kernel, dim3(nb), dim3(256), 0, s, a, target, n, part);
+        hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(64), 0, s, part, nb, n, loss, k0 > 0 ? 1 : 0);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? NLDPC_OK : hip_fail(e, "bce_loss_kernel launch");
