@@ -106,6 +106,17 @@ CNPAIR2 = os.environ.get("NLDPC_GEN_CNPAIR2") == "1"
 # v_add_u32 per row copy instead of an add and a shift-add): cfg3 kernel 51.7 -> 50.9 ms (default 1; Neural and MS kernels only: QMS 169 -> 198 ms with it)
 ROADDR = os.environ.get("NLDPC_GEN_ROADDR", "1") == "1"
 
+# SAVE kernels: the v2c messages saved for the backward are copied from the check-ordered LDS image in
+# 16-byte pieces after the write phase (1, default: one extra barrier per chunk) instead of one store
+# per message and lane copy in the write phase (0: byte stores for QMS, issue-bound -- the cfg5 forward's
+# write phases were 81K of 125K cycles per iteration, profiles/r3f_stamps.txt)
+SAVECOPY = os.environ.get("NLDPC_GEN_SAVECOPY", "1") == "1"
+
+# backward check nodes: weight-gradient sums per lane copy q, added over the row's copies by lane 0 in LDS
+# (1, default: no per-lane accumulator lives across the copies -- QMS z=384 with 3 chunks 3135 -> 16
+# spilled VGPRs) or per-lane accumulators over the copies, one wave sum per row (0)
+GWQ = os.environ.get("NLDPC_GEN_GWQ", "1") == "1"
+
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
 
@@ -165,7 +176,9 @@ def balance(items, weight, P):
 
 
 class Spec:
-    def __init__(self, tag, hb, Z, G, P, Q, pipe=False):
+    def __init__(self, tag, hb, Z, G, P, Q, pipe=False, stage=0):
+        """stage (backward kernels): bytes per message of the saved v2c staged in LDS beside the chunk
+        image (4 fp32, 1 QMS int8 codes; 0 = none, the check nodes gather from global memory)."""
         assert Z % Q == 0
         self.tag, self.hb, self.Z, self.G, self.P, self.Q = tag, hb, Z, G, P, Q
         self.pipe = pipe
@@ -216,22 +229,51 @@ class Spec:
         assert self.threads <= 1024, (tag, self.threads)
         GL = self.G_lds
         cap = ((LDS_BYTES - 4 * GL * app_words(self.N, Z)) // (4 * GL) - 32) // Z
+        row_max = max(len(r) for r in self.row_edges)
         if pipe:  # two buffers; only the count-only counters (G*128 B) share the remaining KiB
             cap = ((160 * 1024 - 1024 - 4 * GL * app_words(self.N, Z)) // (8 * GL) - (32 if GL > 1 else 0)) // Z
-        self.chunks = []  # (row_begin, row_end, edge_begin, edge_end)
-        r0 = 0
-        while r0 < self.M:
-            e0 = self.row_edges[r0][0]
-            r1 = r0
-            while r1 < self.M and self.row_edges[r1][-1] - e0 + 1 <= cap:
-                r1 += 1
-            if r1 == r0:
-                raise SystemExit(f"{tag}: a single check row does not fit in LDS")
-            self.chunks.append((r0, r1, e0, self.row_edges[r1 - 1][-1] + 1))
-            r0 = r1
-        self.chunk_floats = max(e1 - e0 for _, _, e0, e1 in self.chunks) * Z
-        if GL > 1:  # codeword stride = 1 (mod 32 banks) so lanes of different codewords do not collide
-            self.chunk_floats += (1 - self.chunk_floats) % 32
+
+        def chunking(cap, stage):
+            chunks, r0 = [], 0  # (row_begin, row_end, edge_begin, edge_end)
+            while r0 < self.M:
+                e0 = self.row_edges[r0][0]
+                r1 = r0
+                while r1 < self.M and self.row_edges[r1][-1] - e0 + 1 <= cap:
+                    r1 += 1
+                if r1 == r0:
+                    return None
+                chunks.append((r0, r1, e0, self.row_edges[r1 - 1][-1] + 1))
+                r0 = r1
+            cf = max(e1 - e0 for _, _, e0, e1 in chunks) * Z
+            if GL > 1:  # codeword stride = 1 (mod 32 banks) so lanes of different codewords do not collide
+                cf += (1 - cf) % 32
+            # staged saved messages: one region per codeword, 16-byte aligned
+            sf = -(-(max(e1 - e0 for _, _, e0, e1 in chunks) * Z * stage) // 16) * 4 if stage else 0
+            return chunks, cf, sf
+
+        if stage:  # the largest chunks whose image and staged messages fit beside each other
+            c = cap
+            while c >= row_max:
+                got = chunking(c, stage)
+                if got and (got[1] + got[2]) * 4 * GL <= LDS_BYTES - 4 * GL * app_words(self.N, Z):
+                    break
+                c -= 1
+            else:
+                stage = 0  # a row and its staged messages do not fit: gather from global memory
+            if stage:
+                cap = c
+        got = chunking(cap, stage)
+        if got is None:
+            raise SystemExit(f"{tag}: a single check row does not fit in LDS")
+        self.chunks, self.chunk_floats, self.stage_floats = got
+        self.stage = stage
+        # LDS-DMA width of the staging: 16 B when every chunk's block (and the per-codeword stride of
+        # the saved buffer) is a multiple of 16 B, else 4 B
+        blocks = [(e0 * Z * stage, (e1 - e0) * Z * stage) for _, _, e0, e1 in self.chunks] + [(0, self.E * Z * stage)]
+        self.stage_width = 16 if stage and all(o % 16 == 0 and n % 16 == 0 for o, n in blocks) else \
+            4 if stage and all(o % 4 == 0 and n % 4 == 0 for o, n in blocks) else 0
+        if stage and not self.stage_width:
+            self.stage, self.stage_floats = 0, 0
         self.nbuf = 2 if pipe else 1
         self.cn_rows = [balance(list(range(r0, r1)), lambda i: len(self.row_edges[i]), P)
                         for (r0, r1, _, _) in self.chunks]
@@ -532,13 +574,15 @@ def emit(S: Spec) -> str:
             for q in range(Q):
                 for k, e in mine:
                     w(f"    {own_lv(e, q, e0)} = {ref(p, q, k)};")
-                    w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(p, q, k)}, a.qbit);")
+                    if not SAVECOPY:
+                        w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(p, q, k)}, a.qbit);")
             if d1:  # v2c = (0 + xin) + 0: no other edge in the column (bypass: the check node reads xa)
                 w("    if constexpr (!D1_BYPASS) {")
             for j, e in d1:
                 for q in range(Q):
                     w(f"    {{ const float v_ = fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f); "
-                      f"{own_lv(e, q, e0)} = v_; if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qbit); }}")
+                      f"{own_lv(e, q, e0)} = v_; " +
+                      ("}" if SAVECOPY else f"if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qbit); }}"))
             if d1:
                 w("    }")
             w("}")
@@ -749,6 +793,47 @@ def emit(S: Spec) -> str:
                         w("    __builtin_amdgcn_sched_barrier(0);")
             w("}")
 
+    # ---------------------------------------------------------------- SAVE: chunk image -> saved v2c
+    # The image of chunk c is [G][CF] floats in check order: edge e0+i's message for check copy h at
+    # i*Z + h, the saved buffer's layout for this codeword's edges e0..e1 (nldpc_forward.hip).  Every
+    # thread of the workgroup copies 16-byte pieces (QMS: 16 messages -> 16 int8 codes).
+    if not S.pipe and SAVECOPY:
+        for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
+            NE = (e1c - e0c) * Z
+            w("template <int KIND>")
+            w(f"__device__ __forceinline__ void save_c{ci}(const float* lds_all, char* svb, int nlive, int qbit) {{")
+            w("    const int t = threadIdx.x;")
+            w("    (void)qbit;")
+            for g in range(G):
+                src = f"(lds_all + {g * CF * S.nbuf})"
+                w(f"    if ({g} < nlive) {{")
+                w("        if constexpr (KIND == NLDPC_QMS) {")
+                w(f"            int8_t* dst = (int8_t*)(svb + {(g * S.E + e0c) * Z});")
+                if NE % 16 == 0 and (g * CF * S.nbuf) % 4 == 0 and ((g * S.E + e0c) * Z) % 16 == 0:
+                    w(f"            for (int i = t; i < {NE // 16}; i += {S.threads}) {{")
+                    w(f"                const float4* s4 = (const float4*)({src} + 16 * i);")
+                    w("                uint32_t o[4];")
+                    w("#pragma unroll")
+                    w("                for (int k = 0; k < 4; ++k) {")
+                    w("                    const float4 v = s4[k];")
+                    w("                    o[k] = ((uint32_t)qms_code(v.x, qbit) & 255u) | (((uint32_t)qms_code(v.y, qbit) & 255u) << 8) |")
+                    w("                           (((uint32_t)qms_code(v.z, qbit) & 255u) << 16) | ((uint32_t)qms_code(v.w, qbit) << 24);")
+                    w("                }")
+                    w("                reinterpret_cast<uint4*>(dst)[i] = make_uint4(o[0], o[1], o[2], o[3]);")
+                    w("            }")
+                else:
+                    w(f"            for (int i = t; i < {NE}; i += {S.threads}) dst[i] = (int8_t)qms_code({src}[i], qbit);")
+                w("        } else {")
+                w(f"            float* dst = (float*)(svb + {4 * (g * S.E + e0c) * Z});")
+                if NE % 4 == 0 and (g * CF * S.nbuf) % 4 == 0:
+                    w(f"            for (int i = t; i < {NE // 4}; i += {S.threads}) "
+                      f"reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>({src})[i];")
+                else:
+                    w(f"            for (int i = t; i < {NE}; i += {S.threads}) dst[i] = {src}[i];")
+                w("        }")
+                w("    }")
+            w("}")
+
     # ---------------------------------------------------------------- the kernel
     def each_part(fmt, indent="        "):
         for p in PARTS or range(S.P):
@@ -768,7 +853,10 @@ def emit(S: Spec) -> str:
         nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
         w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
-          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw, bool dup_) {{")
+          f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw, bool dup_, "
+          f"const float* lds_all) {{")
+        if S.pipe and SAVECOPY:
+            w("    static_assert(MODE != 1, \"the SAVE kernels use the one-buffer schedule (save_c)\");")
         for i in range(NP(p)):
             w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
         for i in range(NS(p)):
@@ -868,6 +956,8 @@ def emit(S: Spec) -> str:
         w("        const char* svp = SAVE ? a.sv2c + it * a.sv2c_stride * SB : nullptr;")
         w(f"        const rsrc_t sv = make_rsrc((const float*)(svp ? svp + blk * {S.E * Z} * SB : nullptr), "
           f"svp ? nlive * {S.E * Z} * SB : 0);")
+        w(f"        char* svb = svp ? const_cast<char*>(svp) + blk * {S.E * Z} * SB : nullptr;  // (save_c)")
+        w("        (void)sv; (void)svb;")
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
         stamp(1)
         def preload(ci):
@@ -919,6 +1009,8 @@ def emit(S: Spec) -> str:
                 op_w(ci)
                 stamp(2 + 3 * ci)
                 w("        __syncthreads();")
+                if SAVECOPY:  # the image holds the chunk's v2c: save it before the check nodes overwrite it
+                    w(f"        if constexpr (SAVE) {{ if (svb) save_c{ci}<KIND>(lds_all, svb, nlive, a.qbit); __syncthreads(); }}")
                 op_cn(ci)
                 stamp(3 + 3 * ci)
                 w("        __syncthreads();")
@@ -965,7 +1057,7 @@ def emit(S: Spec) -> str:
         w("}")
     w("template <int KIND, int MODE>")
     w("__device__ __forceinline__ void kernel_body(const FusedArgs& a) {")
-    w(f"    __shared__ float lds_all[{CF * S.G_lds * S.nbuf}];")
+    w(f"    __shared__ __attribute__((aligned(16))) float lds_all[{CF * S.G_lds * S.nbuf}];")
     w("    const int t = threadIdx.x;")
     w(f"    // every wave lies in one part ({S.lanes_pad} threads per part): the part is wave-uniform")
     w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes_pad});")
@@ -992,7 +1084,7 @@ def emit(S: Spec) -> str:
     w(f"    __shared__ uint32_t app_all[{S.G_lds * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
     w(f"    uint32_t* appw = app_all + (dup_ ? {G} : g) * {S.N * S.WZX};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
-    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_)",
+    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_, lds_all)",
               indent="    ")
     w("    if constexpr (CNT) {")
     w("        __syncthreads();")
@@ -1013,13 +1105,13 @@ def emit(S: Spec) -> str:
     return "\n".join(L)
 
 
-def emit_bwd(S: Spec) -> str:
+def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     """Backward kernels (training): the forward's ownership and LDS exchange, run in reverse.
 
     State: dL/dc2v_{k+1} of every register edge copy (the forward's c2v slots), one float array per
     lane copy.  Per iteration k = T-1..0: owners write the state into the check-ordered LDS image
-    (degree-1 edges: dL/dy_k * mask_k), the check-node threads gather v2c_k from the saved buffer at
-    the cyclic shift, run cn_backward (nldpc_node.h, the streaming cnb_kernel's arithmetic) and put
+    (degree-1 edges: dL/dy_k * mask_k), the check-node threads read v2c_k (saved in check order; staged
+    into LDS per chunk when S.stage) at their check copy, run cn_backward (nldpc_node.h, the streaming cnb_kernel's arithmetic) and put
     dL/dv2c_k back in place, owners read it back; then the variable-node step: dL/dc2v_k = dL/dy_{k-1}
     * mask_{k-1} + sum of the column's other dL/dv2c_k (prefix + suffix, as vnb_kernel), and the
     cumulative VN-weight chain (carry per channel value).  Weight gradients: per-wave partial sums."""
@@ -1029,8 +1121,8 @@ def emit_bwd(S: Spec) -> str:
     w = L.append
     CF = S.chunk_floats
     w(f"// ---- {S.tag} backward: {S.threads} threads, {WP} wave(s) per part")
-    w(f"namespace fusedb_{S.tag} {{")
-    w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {N}, E = {E}, WP = {WP};")
+    w(f"namespace {ns}_{S.tag} {{")
+    w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {N}, E = {E}, WP = {WP}, MDC = {S.max_dc};")
 
     def X(j, q):
         return 4 * (j * Z + q * ZT)
@@ -1147,98 +1239,152 @@ def emit_bwd(S: Spec) -> str:
             s0 += d
         w("}")
 
-    # ---------------------------------------------------------------- check-node backward (table driven)
-    tab, rowid, shifts, groups = [], [], [], {}
-    for p in range(S.P):
-        for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
-            gl = []
-            rows = S.cn_rows[ci][p]
-            for dc in sorted({len(S.row_edges[i]) for i in rows}, reverse=True):
-                sel = [i for i in rows if len(S.row_edges[i]) == dc]
-                gl.append((dc, len(tab), len(sel)))
-                tab += [S.row_edges[i][0] for i in sel]
-                rowid += sel
-            groups[(p, ci)] = gl
-    w(f"static __constant__ int32_t cn_tab[{max(1, len(tab))}] = {{{', '.join(str(x) for x in tab) or '0'}}};")
-    w(f"static __constant__ int32_t cn_row[{max(1, len(rowid))}] = {{{', '.join(str(x) for x in rowid) or '0'}}};")
-    w(f"static __constant__ int32_t e_shift[{E}] = {{{', '.join(str(int(x)) for x in S.shift)}}};")
+    # ---------------------------------------------------------------- check-node backward
+    # The saved v2c of an iteration is check-ordered ([E][Z] by check copy h), so a chunk's messages are
+    # one contiguous block: with S.stage the block is copied into LDS beside the chunk image by LDS-DMA
+    # (global_load_lds, issued at the start of the chunk's write phase, landed by the barrier before the
+    # check nodes), and each check copy reads its row's messages from LDS at h -- no global gathers in
+    # the check-node phase.  Without staging they are read from global memory at h (coalesced).
+    SBY = S.stage
     w("template <int KIND, int DC>")
-    w("__device__ __forceinline__ void cnb_rows(float* lds, int u, const FusedBwdArgs& a, int it, int t0, int n, "
-      "int e0c, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_) {")
-    w("    asm volatile(\"\" : \"+v\"(u));")
-    w("    for (int r = 0; r < n; ++r) {")
-    w("        const int e0 = cn_tab[t0 + r];")
-    w("        float* rp = lds + (e0 - e0c) * Z + u;")
-    w("        float wv[DC], bv[DC];")
-    w("        int sh[DC];")
-    w("        const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + e0) : nullptr;")
-    w("        const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + e0) : nullptr;")
-    w("        if (KIND == NLDPC_NEURAL || wc) {")
+    w("__device__ __forceinline__ void cnb_row(float* rp, const char* sq, int u, const FusedBwdArgs& a, int it, "
+      "int e0, int row, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
+    w("    __builtin_amdgcn_sched_barrier(0);  // one row at a time (register pressure)")
+    w("    float wv[DC], bv[DC];")
+    w("    const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + e0) : nullptr;")
+    w("    const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + e0) : nullptr;")
+    w("    if (KIND == NLDPC_NEURAL || wc) {")
     w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) wv[k] = wc[k];")
-    w("        } else {")
+    w("        for (int k = 0; k < DC; ++k) wv[k] = wc[k];")
+    w("    } else {")
     w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) wv[k] = 1.f;")
-    w("        }")
-    w("        if (KIND == NLDPC_NEURAL) {")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) bv[k] = bs[k];")
-    w("        } else {")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) bv[k] = 0.f;")
-    w("        }")
-    w("#pragma unroll")
-    w("        for (int k = 0; k < DC; ++k) sh[k] = e_shift[e0 + k];")
-    w("        float gwa[DC], gba[DC];")
-    w("#pragma unroll")
-    w("        for (int k = 0; k < DC; ++k) gwa[k] = gba[k] = 0.f;")
-    w("#pragma unroll")
-    w(f"        for (int q = 0; q < {Q}; ++q) {{")
-    w("            auto load_m = [&](int k) {  // saved v2c of edge k at variable copy (h + s) mod Z, h = u + q*ZT")
-    w("                int t = u + q * ZT + sh[k];")
-    w("                t -= t >= Z ? Z : 0;")
-    w("                if constexpr (KIND == NLDPC_QMS)")
-    w("                    return qms_decode((int8_t)bload8(svr, (vcw >> 2) + (uint32_t)t, (e0 + k) * Z));")
-    w("                else")
-    w("                    return bload(svr, vcw + 4u * (uint32_t)t, 4 * (e0 + k) * Z);")
-    w("            };")
-    w("            if constexpr (KIND == NLDPC_SP) {")
-    w("                float m[DC], gc[DC], gm[DC], gw[DC], gu[DC], gb[DC];")
-    w("#pragma unroll")
-    w("                for (int k = 0; k < DC; ++k) {")
-    w("                    m[k] = load_m(k);")
-    w("                    gc[k] = rp[k * Z + q * ZT];")
-    w("                }")
-    w("                cn_backward<DC, KIND, false>(m, gc, DC, 0.f, wv, wv, bv, wc != nullptr, false, a.qbit, a.lo, a.hi, "
-      "gm, gw, gu, gb, SpRow{a.sp_plan + cn_row[t0 + r] * kSpPlanBytes, a.tanh});")
-    w("#pragma unroll")
-    w("                for (int k = 0; k < DC; ++k) {")
-    w("                    rp[k * Z + q * ZT] = gm[k];")
-    w("                    gwa[k] += gw[k];")
-    w("                }")
-    w("            } else {")
-    w("                cn_bwd_ms<DC, KIND>(load_m, rp + q * ZT, Z, wv, bv, KIND == NLDPC_NEURAL || wc, a.qbit, a.lo, a.hi, "
-      "gwa, gba);")
-    w("            }")
-    w("            __builtin_amdgcn_sched_barrier(0);  // one check copy at a time: the state owns the registers")
-    w("        }")
-    w("        if (a.p_cn) {")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) { const float s_ = wave_sum(dup_ ? 0.f : gwa[k]); if (lane0) a.p_cn[pc + e0 + k] = s_; }")
-    w("        }")
-    w("        if (KIND == NLDPC_NEURAL && a.p_bias) {")
-    w("#pragma unroll")
-    w("            for (int k = 0; k < DC; ++k) { const float s_ = wave_sum(dup_ ? 0.f : gba[k]); if (lane0) a.p_bias[pc + e0 + k] = s_; }")
-    w("        }")
+    w("        for (int k = 0; k < DC; ++k) wv[k] = 1.f;")
     w("    }")
+    w("    if (KIND == NLDPC_NEURAL) {")
+    w("#pragma unroll")
+    w("        for (int k = 0; k < DC; ++k) bv[k] = bs[k];")
+    w("    } else {")
+    w("#pragma unroll")
+    w("        for (int k = 0; k < DC; ++k) bv[k] = 0.f;")
+    w("    }")
+    if not GWQ:
+        w("    float gwa[DC], gba[DC];")
+        w("#pragma unroll")
+        w("    for (int k = 0; k < DC; ++k) gwa[k] = gba[k] = 0.f;")
+    w("#pragma unroll")
+    w(f"    for (int q = 0; q < {Q}; ++q) {{")
+    if GWQ:  # per-copy partial sums (slot q of the wave's Q): no accumulator lives across the copies
+        w("        float gwa[DC], gba[DC];")
+        w("#pragma unroll")
+        w("        for (int k = 0; k < DC; ++k) gwa[k] = gba[k] = 0.f;")
+    w("        auto load_m = [&](int k) {  // saved v2c of edge k at check copy h = u + q*ZT")
+    if SBY:
+        w("            if constexpr (KIND == NLDPC_QMS)")
+        w(f"                return qms_decode(((const int8_t*)sq)[k * {Z} + q * {ZT}]);")
+        w("            else")
+        w(f"                return ((const float*)sq)[k * {Z} + q * {ZT}];")
+    else:
+        w("            if constexpr (KIND == NLDPC_QMS)")
+        w("                return qms_decode((int8_t)bload8(svr, (vcw >> 2) + (uint32_t)(u + q * ZT), (e0 + k) * Z));")
+        w("            else")
+        w("                return bload(svr, vcw + 4u * (uint32_t)(u + q * ZT), 4 * (e0 + k) * Z);")
+    w("        };")
+    w("        if constexpr (KIND == NLDPC_SP) {")
+    w("            float m[DC], gc[DC], gm[DC], gw[DC], gu[DC], gb[DC];")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) {")
+    w("                m[k] = load_m(k);")
+    w("                gc[k] = rp[k * Z + q * ZT];")
+    w("            }")
+    w("            cn_backward<DC, KIND, false>(m, gc, DC, 0.f, wv, wv, bv, wc != nullptr, false, a.qbit, a.lo, a.hi, "
+      "gm, gw, gu, gb, SpRow{a.sp_plan + row * kSpPlanBytes, a.tanh});")
+    w("#pragma unroll")
+    w("            for (int k = 0; k < DC; ++k) {")
+    w("                rp[k * Z + q * ZT] = gm[k];")
+    w("                gwa[k] += gw[k];")
+    w("            }")
+    w("        } else {")
+    w("            cn_bwd_ms<DC, KIND>(load_m, rp + q * ZT, Z, wv, bv, KIND == NLDPC_NEURAL || wc, a.qbit, a.lo, a.hi, "
+      "gwa, gba);")
+    w("        }")
+    def flush(indent):
+        w(f"{indent}if (a.p_cn) {{")
+        w("#pragma unroll")
+        w(f"{indent}    for (int k = 0; k < DC; ++k) {{ const float s_ = wave_sum(dup_ ? 0.f : gwa[k]); "
+          f"if (lane0) a.p_cn[pc + e0 + k] = s_; }}")
+        w(f"{indent}}}")
+        w(f"{indent}if (KIND == NLDPC_NEURAL && a.p_bias) {{")
+        w("#pragma unroll")
+        w(f"{indent}    for (int k = 0; k < DC; ++k) {{ const float s_ = wave_sum(dup_ ? 0.f : gba[k]); "
+          f"if (lane0) a.p_bias[pc + e0 + k] = s_; }}")
+        w(f"{indent}}}")
+
+    def flush_q(indent):  # this copy's wave sums, added up over the row's copies by lane 0 in LDS
+        for arr, dst, off, cond in (("gwa", "a.p_cn", "0", "a.p_cn"), ("gba", "a.p_bias", "MDC", "KIND == NLDPC_NEURAL && a.p_bias")):
+            w(f"{indent}if ({cond}) {{")
+            w("#pragma unroll")
+            w(f"{indent}    for (int k = 0; k < DC; ++k) {{")
+            w(f"{indent}        const float s_ = wave_sum(dup_ ? 0.f : {arr}[k]);")
+            if Q == 1:
+                w(f"{indent}        if (lane0) {dst}[pc + e0 + k] = s_;")
+            else:
+                w(f"{indent}        if (lane0) {{")
+                w(f"{indent}            if (q == 0) gacc[{off} + k] = s_;")
+                w(f"{indent}            else if (q < {Q - 1}) gacc[{off} + k] = gacc[{off} + k] + s_;")
+                w(f"{indent}            else {dst}[pc + e0 + k] = gacc[{off} + k] + s_;")
+                w(f"{indent}        }}")
+            w(f"{indent}    }}")
+            w(f"{indent}}}")
+    if GWQ:
+        flush_q("        ")
+    w("        __builtin_amdgcn_sched_barrier(0);  // one check copy at a time: the state owns the registers")
+    w("    }")
+    if not GWQ:
+        flush("    ")
     w("}")
+    for p in range(S.P):
+        for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
+            w("template <int KIND>")
+            w(f"__device__ __forceinline__ void cnb_p{p}_c{ci}(float* lds, const char* stg, int u, const FusedBwdArgs& a, "
+              "int it, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
+            w("    asm volatile(\"\" : \"+v\"(u));")
+            w("    constexpr int SB = saved_msg_bytes<KIND>();")
+            rows = sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i]))
+            for i in rows:
+                es = S.row_edges[i]
+                off = (es[0] - e0c) * Z
+                w(f"    cnb_row<KIND, {len(es)}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, svr, vcw, pc, "
+                  "lane0, dup_, gacc);")
+            w("}")
+            # the chunk's saved block -> this codeword's staging region (all threads of the workgroup)
+            if SBY and p == 0:
+                nb = (e1c - e0c) * Z * SBY
+                W_ = S.stage_width
+                w("template <int KIND>")
+                w(f"__device__ __forceinline__ void stage_c{ci}(const FusedBwdArgs& a, int it, int64_t blk, int nlive, "
+                  "char* stg_all) {")
+                w(f"    const int t = threadIdx.x, lane = t & 63, w0 = t & ~63;")
+                w(f"    constexpr int NP = {nb // W_};  // {W_}-byte pieces")
+                w(f"    const char* src = a.sv2c + ((int64_t)it * a.sv2c_stride + blk * {E * Z}) * {SBY} + {e0c * Z * SBY};")
+                w("#pragma unroll")
+                w(f"    for (int g = 0; g < {G}; ++g) {{")
+                w("        if (g >= nlive) break;")
+                w(f"        const char* sg = src + (int64_t)g * {E * Z * SBY};")
+                w(f"        char* dg = stg_all + g * {4 * S.stage_floats};")
+                w(f"        for (int i = w0; i < NP; i += {S.threads}) {{")
+                w(f"            if (i + lane < NP) __builtin_amdgcn_global_load_lds((gptr_t)(sg + (int64_t)(i + lane) * {W_}), "
+                  f"(lptr_t)(dg + i * {W_}), {W_}, 0, 0);")
+                w("        }")
+                w("    }")
+                w("}")
 
     # ---------------------------------------------------------------- per-part driver
     for p in range(S.P):
         sp = max(len(S.slots[p]), 1)
         w("template <int KIND>")
         w(f"__device__ __forceinline__ void bwd_p{p}(const FusedBwdArgs& a, float* lds, int u, int64_t blk, int nlive, "
-          f"uint32_t vo, uint32_t vm, uint32_t vcw, int slot, bool lane0, bool dup_) {{")
+          f"uint32_t vo, uint32_t vm, uint32_t vcw, int slot, bool lane0, bool dup_, const char* stg, char* stg_all, "
+          f"float* gacc) {{")
         for q in range(Q):
             w(f"    float g{q}[{sp}];")
         w(f"    const rsrc_t cyr = make_rsrc(a.carry ? a.carry + blk * {NZ} : nullptr, a.carry ? nlive * {4 * NZ} : 0);")
@@ -1275,25 +1421,48 @@ def emit_bwd(S: Spec) -> str:
         w("        const cfloat_p wvn = a.w_vn ? (cfloat_p)(a.w_vn + (int64_t)it * N) : nullptr;")
         w("        const int64_t pc = ((int64_t)it * a.nslots + slot) * E;")
         w("        const int64_t pv = ((int64_t)it * a.nslots + slot) * N;")
+        def bstamp(ph):  # diagnostic stamp build: arrival of each wave at the end of a phase
+            if STAMPS:
+                assert ph < 16
+                w(f"        if (a.stamps && blockIdx.x < 256 && (threadIdx.x & 63) == 0) "
+                  f"a.stamps[((blockIdx.x * {S.threads // 64} + (threadIdx.x >> 6)) * a.T + it) * 16 + {ph}] = "
+                  f"__builtin_amdgcn_s_memtime();")
+        bstamp(0)
         for ci in range(len(S.chunks)):
+            if SBY:  # the chunk's saved messages start moving into LDS now and land by the barrier
+                w(f"        stage_c{ci}<KIND>(a, it, blk, nlive, stg_all);")
             w(f"        wrb_p{p}_c{ci}<KIND>({state_args()}, lds, u, gr, mr, vo, vm);")
+            bstamp(1 + 3 * ci)
+            if SBY:
+                w("        asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // (LDS-DMA: not in hipcc's count)")
             w("        __syncthreads();")
-            for dc, t0, n in groups[(p, ci)]:
-                w(f"        cnb_rows<KIND, {dc}>(lds, u, a, it, {t0}, {n}, {S.chunks[ci][2]}, svr, vcw, pc, lane0, dup_);")
+            w(f"        cnb_p{p}_c{ci}<KIND>(lds, stg, u, a, it, svr, vcw, pc, lane0, dup_, gacc);")
+            bstamp(2 + 3 * ci)
             w("        __syncthreads();")
             w(f"        rdb_p{p}_c{ci}<KIND>({state_args()}, lds, u, a, it, vo, xr, sxp, cyr, wvn, pv, lane0, dup_);")
+            bstamp(3 + 3 * ci)
             w("        __syncthreads();")
         w("        const float* gq_ = it >= 1 ? a.gy.p[it - 1] : nullptr;  // dL/dy_{k-1}")
         w("        const uint8_t* mq_ = (a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t gr1 = {rs('gq_', 4, NZ)};")
         w(f"        const rsrc_t mr1 = {rs('mq_', 1, NZ)};")
         w(f"        vnb_p{p}<KIND>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0, dup_);")
+        bstamp(1 + 3 * len(S.chunks))
         w("    }")
         w("}")
 
     w("template <int KIND>")
     w("__device__ __forceinline__ void bwd_body(const FusedBwdArgs& a) {")
-    w(f"    __shared__ float lds_all[{CF * S.G_lds}];")
+    STF = S.stage_floats
+    if SBY:
+        w(f"    static_assert(saved_msg_bytes<KIND>() == {SBY}, \"kernel built for another saved-message width\");")
+    GA = 2 * S.max_dc * (S.threads // 64) if GWQ and Q > 1 else 1
+    assert 4 * (STF * S.G_lds + CF * S.G_lds + GA) <= 160 * 1024, S.tag
+    w(f"    __shared__ __attribute__((aligned(16))) float lds_sh[{STF * S.G_lds + CF * S.G_lds + GA}];  // staging | images | sums")
+    w(f"    char* stg_all = (char*)lds_sh;  // [G_lds][{4 * STF}] bytes: the chunk's saved messages (S.stage)")
+    w(f"    float* lds_all = lds_sh + {STF * S.G_lds};")
+    w(f"    float* gacc = lds_sh + {STF * S.G_lds + CF * S.G_lds} + {2 * S.max_dc if GA > 1 else 0} * (threadIdx.x >> 6);  "
+      "// this wave's weight-gradient sums over a row's copies (lane 0)")
     w("    const int t = threadIdx.x;")
     w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes_pad});")
     w(f"    const int r0_ = t - p * {S.lanes_pad};")
@@ -1309,8 +1478,12 @@ def emit_bwd(S: Spec) -> str:
     w("    const int slot = blockIdx.x * WP + __builtin_amdgcn_readfirstlane(r0_ >> 6);")
     w("    const bool lane0 = (t & 63) == 0;")
     w(f"    float* lds = lds_all + (dup_ ? {G} : g) * {CF};  // (repeating lanes: their own region)")
+    w(f"    const char* stg = stg_all + (dup_ ? {G} : g) * {4 * STF};")
+    if SBY and S.padded:  # the repeating lanes' staging region is never filled: zeros, not stale LDS
+        w(f"    for (int i = t; i < {STF}; i += {S.threads}) ((float*)(stg_all + {G * 4 * STF}))[i] = 0.f;")
     for p in range(S.P):
-        w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0, dup_);")
+        w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0, dup_, "
+          "stg, stg_all, gacc);")
     w("}")
     w("template <int KIND>")
     w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void bwd_kernel(FusedBwdArgs a) {{")
@@ -1319,6 +1492,12 @@ def emit_bwd(S: Spec) -> str:
     w("}  // namespace")
     return "\n".join(L)
 
+
+# Backward kernels by kind: bytes per staged saved message (Spec stage) and their namespace.  Neural
+# stages fp32 messages (5 chunks at z=384, no spills); QMS its int8 codes (3 chunks); MS / SP gather from
+# global memory (staged fp32 messages need 5 chunks, and the MS / SP kernels spill there: 2646 VGPRs)
+BWD_STAGE = {0: 0, 1: 0, 2: 1, 3: 4}
+BWD_NS = {0: "fusedbs", 1: "fusedbs", 2: "fusedbq", 3: "fusedb"}
 
 MODES = (0, 1, 2, 3)  # forward kernels: decode / decode + save for backward / count-only (all-zero, LLR > 0) / count-only (general)
 
@@ -1330,16 +1509,18 @@ def jit_source(hb, Z, kind, mode):
     point -- nldpc_fx (MODE 0-3) or nldpc_fxb (mode 4, the backward).  Returns (source, geometry dict)."""
     hb = np.asarray(hb, dtype=np.int64)
     G, P, Q = auto_geometry(hb, Z)
-    S = Spec("jit", hb, Z, G, P, Q, pipe=PIPE and mode in (0, 2, 3))  # the SAVE kernels keep one buffer
+    S = Spec("jit", hb, Z, G, P, Q, pipe=PIPE and mode in (0, 2, 3),  # the SAVE kernels keep one buffer
+             stage=BWD_STAGE[kind] if mode == 4 else 0)  # (backward: staged saved messages)
     L = ["// GENERATED by gen_fused.py jit_source -- do not edit.", "#include <hip/hip_runtime.h>",
-         '#include "nldpc_fused.h"', "namespace nldpc {", emit(S) if mode < 4 else emit_bwd(S), "}  // namespace nldpc"]
+         '#include "nldpc_fused.h"', "namespace nldpc {", emit(S) if mode < 4 else emit_bwd(S, BWD_NS[kind]),
+         "}  // namespace nldpc"]
     lb = f"__launch_bounds__({S.threads}, {(S.threads + 255) // 256})"
     if mode < 4:
         L.append(f'extern "C" __global__ {lb} void nldpc_fx(nldpc::FusedArgs a) {{ '
                  f"nldpc::fused_jit::kernel_body<{kind}, {mode}>(a); }}")
     else:
         L.append(f'extern "C" __global__ {lb} void nldpc_fxb(nldpc::FusedBwdArgs a) {{ '
-                 f"nldpc::fusedb_jit::bwd_body<{kind}>(a); }}")
+                 f"nldpc::{BWD_NS[kind]}_jit::bwd_body<{kind}>(a); }}")
     return "\n".join(L) + "\n", {"G": G, "threads": S.threads, "waves_per_part": S.lanes_pad // 64,
                                  "P": P, "Q": Q, "padded": S.padded}
 
@@ -1397,12 +1578,20 @@ def main():
             src.append("}")
             src.append("}  // namespace nldpc")
             write(f"fused_{S.tag}_s{save}.hip", src)
+        # backward kernels: the fp32-message kinds and QMS (int8 codes) stage their saved messages in LDS
+        # beside chunk images sized for them, so they are two generated namespaces
         src = list(head)
-        src.append(emit_bwd(SB_) if on else "")
+        if on:
+            done = set()
+            for k in kinds:
+                if BWD_NS[k] not in done:
+                    done.add(BWD_NS[k])
+                    src.append(emit_bwd(Spec(S.tag, S.hb, S.Z, S.G, S.P, S.Q, stage=BWD_STAGE[k]), BWD_NS[k]))
         src.append(f"void* fused_{S.tag}_bwd(int kind) {{")
         if on:
             for k in kinds:
-                src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fusedb_{S.tag}::bwd_kernel<{k}>);")
+                nsk = BWD_NS[k]
+                src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&{nsk}_{S.tag}::bwd_kernel<{k}>);")
         src.append("    return nullptr;")
         src.append("}")
         src.append("}  // namespace nldpc")

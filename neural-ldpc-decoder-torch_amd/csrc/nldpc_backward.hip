@@ -19,7 +19,9 @@
 // lines serialised in L2 and bounded both backward kernels before).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "nldpc_fused.h"
 
@@ -235,7 +237,8 @@ __device__ __forceinline__ void cnb_body(const CNBArgs& a, const Geo& q, const i
             const int t = h + a.g.e_shift[beg + k];
             vv[k] = t >= Z ? t - Z : t;
             const int64_t off = (base + beg + k) * Z + vv[k];
-            m[k] = a.v2c_code ? qms_decode(a.v2c_code[off]) : a.v2c[off];
+            const int64_t offh = (base + beg + k) * Z + h;  // saved v2c: check order
+            m[k] = a.v2c_code ? qms_decode(a.v2c_code[offh]) : a.v2c[offh];
             gc[k] = a.gc2v[off];
         } else {
             vv[k] = 0;
@@ -440,6 +443,11 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
     a.carry = a.w_vn ? reinterpret_cast<float*>(wb + W.carry_off) : nullptr;
     a.nslots = W.nslots;
     for (int k = 0; k < kFusedMaxT; ++k) a.gy.p[k] = k < T ? const_cast<float*>(grad_outs[k]) : nullptr;
+    // diagnostic stamp build (lib_stamps/): NLDPC_STAMPS_BWD=<file> collects the phase stamps of each call
+    static const char* stamp_file = std::getenv("NLDPC_STAMPS_BWD");
+    const size_t stamp_n = (size_t)256 * (f.threads / 64) * T * 16;
+    if (stamp_file) NLDPC_HIP_CHECK(hipMalloc(&a.stamps, stamp_n * sizeof(uint64_t)));
+    if (stamp_file) NLDPC_HIP_CHECK(hipMemsetAsync(a.stamps, 0, stamp_n * sizeof(uint64_t), s));
     void* args[] = {&a};
     const int64_t blocks = (B + f.G - 1) / f.G;
     prof_start(PROF_FUSED_BWD, s);
@@ -447,6 +455,18 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
     prof_stop(s);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "fused backward launch");
+    if (stamp_file) {
+        std::vector<uint64_t> h(stamp_n);
+        NLDPC_HIP_CHECK(hipStreamSynchronize(s));
+        NLDPC_HIP_CHECK(hipMemcpy(h.data(), a.stamps, stamp_n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        if (FILE* fp = std::fopen(stamp_file, "wb")) {
+            const int32_t hdr[4] = {256, f.threads / 64, T, 16};
+            std::fwrite(hdr, sizeof(hdr), 1, fp);
+            std::fwrite(h.data(), sizeof(uint64_t), stamp_n, fp);
+            std::fclose(fp);
+        }
+        (void)hipFree(a.stamps);
+    }
     if (a.p_cn) e = reduce_launch(a.p_cn, T, W.nslots, G.E, g_w_cn, s);
     if (e == hipSuccess && a.p_bias) e = reduce_launch(a.p_bias, T, W.nslots, G.E, g_bias, s);
     if (e == hipSuccess && a.p_vn) e = reduce_launch(a.p_vn, T, W.nslots, G.N, g_w_vn, s);
@@ -479,7 +499,9 @@ extern "C" int nldpc_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_
     int st = validate_cfg(g, cfg, B, T);
     if (st) return st;
     if (!xa || !outs || !grad_outs || !saved || !work) return fail(NLDPC_EINVAL, "nldpc_backward: null argument");
-    const bool fusedb = fused_bwd_eligible(g, cfg, T, grad_c2v_out || grad_c2v_in);
+    // (the fused kernels stage the saved messages by 16-byte LDS-DMA: a 16-byte aligned buffer)
+    const bool fusedb = fused_bwd_eligible(g, cfg, T, grad_c2v_out || grad_c2v_in) &&
+                        (reinterpret_cast<uintptr_t>(saved) & 15) == 0;
     const WorkLayout WL = work_layout(g, cfg, B, T);
     if (work_bytes < (fusedb ? fused_work_layout(g, cfg, B, T).total : WL.total))
         return fail(NLDPC_EINVAL, "nldpc_backward: workspace too small");

@@ -10,7 +10,10 @@
 //              at the cyclic shift (h + s_e) mod Z (the reference's lifting_matrix_1 GEMM), does
 //              the min-sum / sum-product update + learned weighting (NeuralLDPCDecoder.py:65-91,
 //              Boosted…py:386-512) and scatters c2v back to the same addresses (lifting_matrix_2).
-// Message state is [B][E][Z] fp32 in HBM with E in C-order; see DESIGN.md for the roofline.
+// Message state is [B][E][Z] fp32 in HBM with E in C-order; see DESIGN.md for the roofline.  The c2v
+// state is indexed by variable copy v; the v2c messages (scratch, and the copies saved for the backward)
+// by check copy h = (v - s_e) mod Z, so the check node reads them unrotated and the fused kernels save
+// and stage them as contiguous blocks of their check-ordered LDS images.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -109,8 +112,11 @@ __device__ __forceinline__ void vn_body(const VNArgs& a, const Geo& q, const int
                 for (int m = k + 1; m < DV; ++m)
                     if (m < d) S = fadd(S, c[m]);
                 const float m = fadd(x0, S);
-                a.v2c[(base + eidx[k]) * Z + v] = m;
-                if (KIND == NLDPC_QMS && a.v2c_code) a.v2c_code[(base + eidx[k]) * Z + v] = (int8_t)qms_code(m, a.qbit);
+                // v2c is kept in CHECK order: slot h = (v - s_e) mod Z is read by check copy h
+                int hh = v - a.g.e_shift[eidx[k]];
+                hh += hh < 0 ? Z : 0;
+                a.v2c[(base + eidx[k]) * Z + hh] = m;
+                if (KIND == NLDPC_QMS && a.v2c_code) a.v2c_code[(base + eidx[k]) * Z + hh] = (int8_t)qms_code(m, a.qbit);
                 P = fadd(P, c[k]);
             }
         }
@@ -131,7 +137,7 @@ __device__ __forceinline__ void cn_body(const CNArgs& a, const Geo& q, const int
         if (k < d) {
             const int t = h + a.g.e_shift[beg + k];
             vv[k] = t >= Z ? t - Z : t;
-            m[k] = a.v2c[(base + beg + k) * Z + vv[k]];
+            m[k] = a.v2c[(base + beg + k) * Z + h];  // (check order: the VN kernel rotated it)
         } else {
             vv[k] = 0;
             m[k] = 0.f;

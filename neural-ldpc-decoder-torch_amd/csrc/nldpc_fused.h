@@ -31,7 +31,7 @@ struct FusedArgs {
     TanhRef tanh;            // torch.tanh table (SP)
     float* c2v_out;      // [B][E][Z] final message state, or nullptr
     // what the backward needs (SAVE kernels only; SavedLayout in nldpc_internal.h)
-    char* sv2c;          // [T][B][E][Z] v2c of every iteration (fp32; QMS: int8 codes, qms_code)
+    char* sv2c;          // [T][B][E][Z] v2c of every iteration by check copy (fp32; QMS: int8 codes, qms_code)
     uint8_t* symask;     // [T][B][N][Z] posterior clamp masks (Boosted), or nullptr
     float* sxin;         // [T][B][N][Z] channel value xin of every iteration (cumulative VN weights), or nullptr
     int64_t sv2c_stride, symask_stride, sxin_stride;  // elements per iteration
@@ -512,7 +512,7 @@ struct FusedBwdArgs {
     const float* w_vn;     // [T][N] or nullptr
     const uint8_t* sp_plan;  // SP product order (DevGraph::sp_plan)
     TanhRef tanh;            // torch.tanh table (SP)
-    const char* sv2c;      // saved [T][B][E][Z] (fp32; QMS: int8 codes)
+    const char* sv2c;      // saved [T][B][E][Z] by check copy (fp32; QMS: int8 codes); 16-byte aligned
     const uint8_t* symask; // saved [T][B][N][Z] or nullptr (Neural)
     const float* sxin;     // saved [T][B][N][Z] or nullptr
     int64_t sv2c_stride, symask_stride, sxin_stride;
@@ -522,8 +522,12 @@ struct FusedBwdArgs {
     float* carry;          // [B][N][Z] VN-chain carry (workspace; written before it is read)
     int64_t nslots;
     OutPtrs gy;            // T output gradients [B][N][Z] (nullptr = zero)
+    uint64_t* stamps;      // diagnostic stamp build only (make STAMPS=1): [256][waves][T][16] s_memtime
 };
 
+// LDS-DMA operands (__builtin_amdgcn_global_load_lds: global source per lane, wave-uniform LDS base)
+typedef __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
 __device__ __forceinline__ uint32_t bload8(rsrc_t r, uint32_t vo, int so) {
     return __builtin_amdgcn_raw_buffer_load_b8(r, vo, so, 0);
 }

@@ -77,11 +77,23 @@ __device__ __forceinline__ bool qms_active_q(int q) { return q == 6 || q == 5 ||
 // Q's clip on m, so QMS saves one signed byte 2*m' per message: m' = Q(m) inside the clip range and
 // sign(m) * (hi + 1) outside it, which gives Q(m') == Q(m) and the same mask (Q's values are
 // multiples of 1/2 with |2 m'| <= 33).  A quarter of the fp32 traffic, both directions.
+// For an active q in nine operations (the saved-state writes are a QMS training forward's hottest VALU
+// work): inside the clip range 2 Q(m) = med3(rint(m s), +-hi s) * 2/s exactly (quantize_active); outside
+// it sign(m) (2 hi + 2); NaN gives -(2 hi + 2) as the definition does (tests/test_qms_code.py checks the
+// identity over every grid boundary and random inputs for every q).
 __device__ __forceinline__ int qms_code(float m, int q) {
     const QRange r = q_range(q);
-    const float qv = quantize(m, q);
-    const float mp = (m >= r.lo && m <= r.hi) ? qv : (m > 0.f ? r.hi + 1.f : -(r.hi + 1.f));
-    return (int)rintf(2.f * mp);
+    if (!r.active) {  // (not used: QMS saves codes only with an active quantiser)
+        const float mp = (m >= r.lo && m <= r.hi) ? quantize(m, q) : (m > 0.f ? r.hi + 1.f : -(r.hi + 1.f));
+        return (int)rintf(2.f * mp);
+    }
+    const float s = q == 5 ? 2.f : (q == 3 ? 0.5f : 1.f);
+    const float k2 = q == 5 ? 1.f : (q == 3 ? 4.f : 2.f);  // 2 / s
+    const float hs = q == 6 ? 15.5f : (q == 5 ? 15.f : (q == -5 ? 15.f : (q == 4 ? 7.f : 3.f)));  // hi * s
+    const float c_out = 2.f * r.hi + 2.f;
+    const float t = fmul(__builtin_amdgcn_fmed3f(rintf(fmul(m, s)), -hs, hs), k2);
+    const float c = fabsf(m) <= r.hi ? t : (m > 0.f ? c_out : -c_out);
+    return (int)c;
 }
 __device__ __forceinline__ float qms_decode(int c) { return 0.5f * (float)c; }
 
