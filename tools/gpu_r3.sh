@@ -1,0 +1,32 @@
+# GPU-box script (run via gpurun; the library is built on the CPU side and travels with the tree):
+# GPU parity tests, smoke, the bench lines of every workload and a rocprofv3 kernel-trace summary of the
+# headline (cfg3) bench.  Every GPU step has its own time limit; the first failing step ends the script.
+# TAG=r3a PHASES="tests smoke cfg3 prof cfg5 cfg2 ucn" bash tools/gpu_r3.sh
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
+TAG=${TAG:-r3}
+PHASES=${PHASES:-"tests smoke cfg3 prof cfg5 cfg2 ucn"}
+cd $R
+export TMPDIR=/tmp
+for s in $PHASES; do
+    echo "== $s $(date +%T)"
+    case $s in
+    tests) timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -x \
+               -p no:cacheprovider > $O/${TAG}_gpu_tests.log 2>&1; rc=$?; tail -3 $O/${TAG}_gpu_tests.log ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1; rc=$? ;;
+    cfg3)  timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $O/${TAG}_bench_cfg3.log 2>&1; rc=$?; tail -c 1500 $O/${TAG}_bench_cfg3.log ;;
+    prof)  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof_cfg3 -o run --output-format csv \
+               -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-sweep > $O/${TAG}_bench_cfg3_under_rocprof.log 2>&1); rc=$? ;;
+    cfg5)  timeout -k 10 600 python -u bench.py --workload cfg5 --steps 5 --warmup 2 > $O/${TAG}_bench_cfg5.log 2>&1; rc=$?; tail -c 800 $O/${TAG}_bench_cfg5.log ;;
+    prof5) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof_cfg5 -o run --output-format csv \
+               -- python3 $R/bench.py --workload cfg5 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_cfg5_under_rocprof.log 2>&1); rc=$? ;;
+    cfg2)  timeout -k 10 300 python -u bench.py --workload cfg2 --steps 50 --warmup 5 --no-cpu-baseline > $O/${TAG}_bench_cfg2.log 2>&1; rc=$?; tail -c 800 $O/${TAG}_bench_cfg2.log ;;
+    ucn)   timeout -k 10 600 python -u bench.py --workload cfg3ucn --steps 5 --warmup 2 --no-cpu-baseline > $O/${TAG}_bench_ucn_MS_112.log 2>&1 &&
+           timeout -k 10 600 python -u bench.py --workload cfg3ucn --kind QMS --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_ucn_QMS_112.log 2>&1; rc=$?
+           tail -c 600 $O/${TAG}_bench_ucn_MS_112.log; tail -c 600 $O/${TAG}_bench_ucn_QMS_112.log ;;
+    ab)    VARIANTS="${VARIANTS}" STEPS=6 bash tools/gpu_ab.sh > $O/${TAG}_ab.txt 2>&1; rc=$?; cat $O/${TAG}_ab.txt ;;
+    *) echo "unknown step $s"; rc=2 ;;
+    esac
+    echo "== $s rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+done
