@@ -117,6 +117,13 @@ SAVECOPY = os.environ.get("NLDPC_GEN_SAVECOPY", "1") == "1"
 # spilled VGPRs) or per-lane accumulators over the copies, one wave sum per row (0)
 GWQ = os.environ.get("NLDPC_GEN_GWQ", "1") == "1"
 
+# NLDPC_GEN_ZADD=0: VN chains start from their first message. The reference's sums start from a 0 (sgemm with 0/1 weights), but
+# 0 + x == x for every x except -0 (-> +0), and the sign of a zero is never observed: the check node treats
+# +-0 alike (not positive, |m| = 0 masked), +-0 posteriors compare equal and give the same hard decision.
+# Default 1 = keep the explicit "0 +" adds: without them (0) the cfg3 kernel measured 1 % SLOWER (48.49 -> 48.94/49.03 ms,
+# profiles/r3b_ab.txt; register allocation), though they are ~2 % of the VALU instructions
+ZADD = os.environ.get("NLDPC_GEN_ZADD", "1") == "1"
+
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
 
@@ -405,7 +412,7 @@ def emit(S: Spec) -> str:
         if not final:
             for T_, arr, xin, g in grp:
                 ch = f"chan2<KIND>({xin}, a)" if T_ == "f2" else f"chan<KIND>({xin}, a)"
-                w(f"            const {T_} x0_{g} = {add(T_, zero(T_), ch)};")
+                w(f"            const {T_} x0_{g} = {add(T_, zero(T_), ch) if ZADD else ch};")
             # edges two at a time: the chains of k and k+1 (S_k from P_{k-1}, S_{k+1} from P_k) run
             # interleaved -- twice the independent adds per wave for the VN's dependent-add tail.
             # Chain k reads c_{k+1} first, before chain k+1 overwrites it with v2c_{k+1}.
@@ -414,9 +421,11 @@ def emit(S: Spec) -> str:
                 w("            {")
                 if two:
                     for T_, arr, xin, g in grp:
-                        w(f"                const {T_} Pk_{g} = {add(T_, f'P_{g}', f'{arr}[{s + k}]')};  // P_k")
+                        pk = f"{arr}[{s + k}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k}]')
+                        w(f"                const {T_} Pk_{g} = {pk};  // P_k")
                     for T_, arr, xin, g in grp:
-                        w(f"                {T_} S_{g} = {add(T_, f'P_{g}', f'{arr}[{s + k + 1}]')};")
+                        s1 = f"{arr}[{s + k + 1}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k + 1}]')
+                        w(f"                {T_} S_{g} = {s1};")
                         w(f"                {T_} U_{g} = Pk_{g};")
                     for m in range(k + 2, d):
                         for T_, arr, xin, g in grp:
@@ -445,7 +454,8 @@ def emit(S: Spec) -> str:
         else:
             for k in range(d):
                 for T_, arr, xin, g in grp:
-                    w(f"            P_{g} = {add(T_, f'P_{g}', f'{arr}[{s + k}]')};")
+                    pk = f"{arr}[{s + k}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k}]')
+                    w(f"            P_{g} = {pk};")
 
     for p in range(S.P):
         cols = S.reg_cols[p]
@@ -580,7 +590,8 @@ def emit(S: Spec) -> str:
                 w("    if constexpr (!D1_BYPASS) {")
             for j, e in d1:
                 for q in range(Q):
-                    w(f"    {{ const float v_ = fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f); "
+                    v1 = f"fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f)" if ZADD else f"chan<KIND>({xref(p, j, q)}, a)"
+                    w(f"    {{ const float v_ = {v1}; "
                       f"{own_lv(e, q, e0)} = v_; " +
                       ("}" if SAVECOPY else f"if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qbit); }}"))
             if d1:
@@ -609,7 +620,7 @@ def emit(S: Spec) -> str:
                         w(f"    {{ const float xo_ = xl_{j}_{q};")
                     else:
                         w(f"    {{ const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
-                    w(f"      const float P_ = fadd(0.f, {own_lv(e, q, e0)});")
+                    w(f"      const float P_ = {'fadd(0.f, ' + own_lv(e, q, e0) + ')' if ZADD else own_lv(e, q, e0)};")
                     w("      float y_;")
                     w("      if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w(f"          bool m_; y_ = posterior_m<KIND>(xo_, P_, a, m_); bstore(pr, vo, {X(j, q)}, y_); "
@@ -766,7 +777,7 @@ def emit(S: Spec) -> str:
                         w("        if constexpr (D1_BYPASS) {")
                         w(f"            const uint32_t dv_ = {dv};")
                         w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, "
-                          f"fadd(cd[{S.cd_index[p].index((e, q))}], fadd(0.f, m{n}[{k}])), ps);")
+                          f"fadd(cd[{S.cd_index[p].index((e, q))}], {'fadd(0.f, m' + str(n) + '[' + str(k) + '])' if ZADD else 'm' + str(n) + '[' + str(k) + ']'}), ps);")
                         w(f"            if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m{n}[{k}]);")
                         w(f"        }} else {{ rq{n}[{k * Z}] = m{n}[{k}]; }}")
                     elif "cnwrite" in SKIP:  # (timing experiment: keep the value live without the LDS write)

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void ber_kernel(const float* llr, const uint8_
 
 // ---------------------------------------------------------------- multi-iteration BCE loss
 constexpr int kBceMaxK = 64;
-constexpr int kBceBlocks = 2048;  // element blocks (workgroups) of the loss pass
+constexpr int kBceBlocks = 16384;  // element blocks (workgroups) of the loss pass
 struct BceArgs {
     const float* x[kBceMaxK];
     float coef[kBceMaxK];
@@ -122,11 +122,14 @@ __device__ __forceinline__ float bce_term(float x, float t) {
 // One workgroup per element block, every term: each thread reads its labels once and the K logits at
 // the same positions (16 B loads), and sums coef_k * term in fp64 (fp32 terms, as torch's); the finish
 // kernel adds the per-block partial sums in a fixed order (deterministic) and divides by n.  (r2 read
-// the labels once per term, twice the bytes at cfg5: 6.7 ms for 8.2 GB of logits.)
+// the labels once per term, twice the bytes at cfg5: 6.7 ms for 8.2 GB of logits.)  r3: the pass is
+// bound by the latency of its dependent chains (exp -> log1p -> fp64 sum), not by HBM: 8x the
+// element blocks (about two float4 of every term per thread, 8 waves per SIMD) and two fp64
+// accumulators (even / odd terms) -- cfg5 7.4 ms -> see DESIGN.md.
 __global__ __launch_bounds__(256) void bce_loss_kernel(BceArgs a, const float* __restrict__ target, int64_t n,
                                                        double* __restrict__ part) {
     __shared__ double red[4];
-    double acc = 0.0;
+    double acc0 = 0.0, acc1 = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool vec = (reinterpret_cast<uintptr_t>(target) & 15) == 0;
@@ -134,28 +137,45 @@ __global__ __launch_bounds__(256) void bce_loss_kernel(BceArgs a, const float* _
     const int64_t n4 = vec ? n / 4 : 0;
     for (int64_t i = i0; i < n4; i += stride) {
         const float4 t = target ? reinterpret_cast<const float4*>(target)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int k = 0; k < a.K; ++k) {
+        int k = 0;
+        for (; k + 1 < a.K; k += 2) {
             const float4 v = reinterpret_cast<const float4*>(a.x[k])[i];
-            acc += (double)a.coef[k] * (((double)bce_term(v.x, t.x) + (double)bce_term(v.y, t.y)) +
-                                        ((double)bce_term(v.z, t.z) + (double)bce_term(v.w, t.w)));
+            const float4 u = reinterpret_cast<const float4*>(a.x[k + 1])[i];
+            acc0 += (double)a.coef[k] * (((double)bce_term(v.x, t.x) + (double)bce_term(v.y, t.y)) +
+                                         ((double)bce_term(v.z, t.z) + (double)bce_term(v.w, t.w)));
+            acc1 += (double)a.coef[k + 1] * (((double)bce_term(u.x, t.x) + (double)bce_term(u.y, t.y)) +
+                                             ((double)bce_term(u.z, t.z) + (double)bce_term(u.w, t.w)));
+        }
+        if (k < a.K) {
+            const float4 v = reinterpret_cast<const float4*>(a.x[k])[i];
+            acc0 += (double)a.coef[k] * (((double)bce_term(v.x, t.x) + (double)bce_term(v.y, t.y)) +
+                                         ((double)bce_term(v.z, t.z) + (double)bce_term(v.w, t.w)));
         }
     }
     for (int64_t i = 4 * n4 + i0; i < n; i += stride) {
         const float t = target ? target[i] : 0.f;
-        for (int k = 0; k < a.K; ++k) acc += (double)a.coef[k] * (double)bce_term(a.x[k][i], t);
+        for (int k = 0; k < a.K; ++k) acc0 += (double)a.coef[k] * (double)bce_term(a.x[k][i], t);
     }
+    double acc = acc0 + acc1;
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
     if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// fixed-order sum of the block partials: 64 lanes each add a contiguous slice, lane 0 adds the slices
 __global__ __launch_bounds__(64) void bce_finish_kernel(const double* __restrict__ part, int nb, int64_t n,
                                                         float* __restrict__ loss, int accumulate) {
+    __shared__ double sl[64];
+    const int per = (nb + 63) / 64;
+    double s = 0.0;
+    for (int b = threadIdx.x * per; b < nb && b < (int)(threadIdx.x + 1) * per; ++b) s += part[b];
+    sl[threadIdx.x] = s;
+    __syncthreads();
     if (threadIdx.x == 0) {
-        double s = 0.0;
-        for (int b = 0; b < nb; ++b) s += part[b];
-        const float v = (float)(s / (double)n);
+        double t = 0.0;
+        for (int l = 0; l < 64; ++l) t += sl[l];
+        const float v = (float)(t / (double)n);
         *loss = accumulate ? *loss + v : v;
     }
 }
@@ -229,8 +249,8 @@ extern "C" int nldpc_bce_workspace(int64_t n, int32_t K, size_t* bytes) {
     return NLDPC_OK;
 }
 
-static int bce_blocks(int64_t n) {  // ~8 float4 of every term per thread, at most kBceBlocks element blocks
-    const int64_t b = (n + 256 * 32 - 1) / (256 * 32);
+static int bce_blocks(int64_t n) {  // ~2 float4 of every term per thread, at most kBceBlocks element blocks
+    const int64_t b = (n + 256 * 8 - 1) / (256 * 8);
     return (int)(b < 1 ? 1 : (b < kBceBlocks ? b : kBceBlocks));
 }
 

@@ -372,6 +372,9 @@ __device__ __forceinline__ void two_smallest_abs3(const float (&m)[DC], float& m
 #ifndef NLDPC_CN_XSIGN
 #define NLDPC_CN_XSIGN 0
 #endif
+#ifndef NLDPC_CN_MAGI
+#define NLDPC_CN_MAGI 0
+#endif
 template <int DC>
 __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
     float min1, min2, mg1, mg2;
@@ -396,6 +399,25 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         mg1 = __builtin_amdgcn_fmed3f(min1, 0.f, 10000.f);  // the masked tile entries (10000) take part
         mg2 = __builtin_amdgcn_fmed3f(min2, 0.f, 10000.f);  // in the min (min1, min2 >= 0: a clamp)
     }
+#if NLDPC_CN_MAGI
+    // the magnitude select without a compare: with a = bits(mg1) <= b = bits(mg2) (non-negative floats
+    // order as integers) and x = bits(|m_k|), t = sat(a + b - x) is b for the edge holding the minimum
+    // (x == bits(min1)) and <= a for every other edge (x >= bits(min2)), so med3(a, b, t) is the
+    // "minimum over the others" -- v_and + v_sub (full rate) + v_med3_u32 instead of v_cmp_eq into an
+    // SGPR pair, the SGPR-read hazard's s_nop and v_cndmask.  (Odd DC, minima capped after tracking:
+    // min1 > 10000 gives a == b; min1 <= 10000 < min2 gives b == 10000 and t == b exactly at x == min1.)
+    // Experiment, off by default: bit-exact, but the cfg3 kernel measured 5 % slower (48.9 -> 51.4 ms,
+    // profiles/r3b_ab.txt) although it issues fewer half-rate instructions.
+    const uint32_t ma_ = __float_as_uint(mg1), mb_ = __float_as_uint(mg2), ms_ = ma_ + mb_;
+    auto magsel = [&](float x) {
+        uint32_t t, r;
+        asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(t) : "v"(ms_), "v"(__float_as_uint(x) & 0x7fffffffu));
+        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(ma_), "v"(mb_), "v"(t));
+        return __uint_as_float(r);
+    };
+#else
+    auto magsel = [&](float x) { return fabsf(x) == min1 ? mg2 : mg1; };
+#endif
 #if NLDPC_CN_XSIGN
     // sign by bit arithmetic (m has no zeros here): the output is positive iff the number of positive
     // OTHER inputs is odd, i.e. its sign bit is sb_k ^ (xor of all sign bits) ^ (DC & 1) -- one v_xor per
@@ -407,11 +429,14 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
     asm volatile("" : "+v"(mg1), "+v"(mg2));
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
+        const float mag = magsel(m[k]);
         const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
-        // r = max(., 0) is +0 or positive (or -0, whose sign bit the OR leaves set: a zero's sign is
-        // never observed by the decoder's sums)
-        m[k] = __uint_as_float(__float_as_uint(r) | ((__float_as_uint(m[k]) ^ xs) & 0x80000000u));
+        // r = max(., 0) is +0 or positive (or -0: a zero's sign is never observed by the decoder's
+        // sums); the sign bit of m_k ^ xs inserted by one v_bfi_b32
+        uint32_t o;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(o) : "v"(0x7fffffffu), "v"(__float_as_uint(r)),
+            "v"(__float_as_uint(m[k]) ^ xs));
+        m[k] = __uint_as_float(o);
     }
 #else
     bool pos[DC];
@@ -424,7 +449,7 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
     asm volatile("" : "+v"(mg1), "+v"(mg2));
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
+        const float mag = magsel(m[k]);
         const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
         m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
     }

@@ -35,6 +35,7 @@ class NeuralLDPCDecoder(nn.Module):
         self.biases_var = nn.ParameterList(
             [nn.Parameter(torch.zeros(E, dtype=torch.float32)) for _ in range(iter_node_counts)])
         self._cfg = DecodeCfg(kind=KIND_NEURAL, keep_state=False)  # forward() never resumes from a state
+        self._wb_cache = None  # (key, w [T, E], b [T, E]) for calls that record no autograd graph
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
                               error_msgs):
@@ -43,10 +44,24 @@ class NeuralLDPCDecoder(nn.Module):
         super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
                                       error_msgs)
 
+    def _weights(self):
+        """The per-iteration weights and biases as [T, E] tensors.  When no autograd graph is recorded
+        (torch.no_grad, or no parameter requires grad) the stacked copies are kept and reused until a
+        parameter changes (storage or in-place version: optimizer steps, load_state_dict), so a serving
+        loop's decode is one kernel launch instead of three."""
+        ps = list(self.weights_var) + list(self.biases_var)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in ps):
+            self._wb_cache = None
+            return torch.stack(list(self.weights_var)), torch.stack(list(self.biases_var))
+        key = tuple((p.data_ptr(), p._version, p.device) for p in ps)
+        if self._wb_cache is None or self._wb_cache[0] != key:
+            with torch.no_grad():
+                self._wb_cache = (key, torch.stack(list(self.weights_var)), torch.stack(list(self.biases_var)))
+        return self._wb_cache[1], self._wb_cache[2]
+
     def forward(self, xa):
         T = self.iter_node_counts
-        w = torch.stack(list(self.weights_var))
-        b = torch.stack(list(self.biases_var))
+        w, b = self._weights()
         outs, _ = decode_autograd(self.conn_mat.graph, self._cfg, xa, T, w_cn=w, bias=b)
         return outs
 
@@ -56,6 +71,5 @@ class NeuralLDPCDecoder(nn.Module):
         errors) per iteration, equal to nldpc.channel.ber_counts(self.forward(xa), y, convention=...)
         without materialising the T posteriors.  y: [B, N*Z] codeword bits or None (all-zero)."""
         T = self.iter_node_counts
-        w = torch.stack(list(self.weights_var))
-        b = torch.stack(list(self.biases_var))
+        w, b = self._weights()
         return decode_count(self.conn_mat.graph, self._cfg, xa, T, w_cn=w, bias=b, y=y, convention=convention)

@@ -25,6 +25,12 @@ for s in $PHASES; do
            timeout -k 10 600 python -u bench.py --workload cfg3ucn --kind QMS --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_ucn_QMS_112.log 2>&1; rc=$?
            tail -c 600 $O/${TAG}_bench_ucn_MS_112.log; tail -c 600 $O/${TAG}_bench_ucn_QMS_112.log ;;
     ab)    VARIANTS="${VARIANTS}" STEPS=6 bash tools/gpu_ab.sh > $O/${TAG}_ab.txt 2>&1; rc=$?; cat $O/${TAG}_ab.txt ;;
+    icache) bash tools/gpu_icache.sh > $O/${TAG}_icache.txt 2>&1; rc=$?; cat $O/${TAG}_icache.txt ;;
+    host)  timeout -k 10 300 python -u tools/dev/host_overhead.py > $O/${TAG}_host_overhead.txt 2>&1; rc=$?; head -30 $O/${TAG}_host_overhead.txt ;;
+    cfg2np) timeout -k 10 300 python -u bench.py --workload cfg2 --steps 500 --warmup 20 --no-cpu-baseline --no-profile --no-count-only > $O/${TAG}_bench_cfg2_noprof.log 2>&1 &&
+           (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof_cfg2 -o run --output-format csv \
+               -- python3 $R/bench.py --workload cfg2 --steps 500 --warmup 20 --no-cpu-baseline --no-profile --no-count-only > $O/${TAG}_bench_cfg2_under_rocprof.log 2>&1); rc=$?
+           tail -c 400 $O/${TAG}_bench_cfg2_noprof.log ;;
     *) echo "unknown step $s"; rc=2 ;;
     esac
     echo "== $s rc=$rc"
