@@ -124,11 +124,31 @@ __device__ __forceinline__ float bce_term(float x, float t) {
 // kernel adds the per-block partial sums in a fixed order (deterministic) and divides by n.  (r2 read
 // the labels once per term, twice the bytes at cfg5: 6.7 ms for 8.2 GB of logits.)  r3: the pass is
 // bound by the latency of its dependent chains (exp -> log1p -> fp64 sum), not by HBM: 8x the
-// element blocks (about two float4 of every term per thread, 8 waves per SIMD) and two fp64
-// accumulators (even / odd terms) -- cfg5 7.4 ms -> see DESIGN.md.
+// element blocks (about two float4 of every term per thread) and two fp64 accumulators (even / odd
+// terms): 7.4 -> 7.0 ms at cfg5; then the grid table above.
+// Logits on the half-integer grid (every QMS decoder output is one: Q(xa) plus quantised check messages,
+// clamped to the QMS range) with a 0/1 label take their term from a per-block table of bce_term at
+// those grid points -- the same function at the same argument, so the same fp32 value -- instead of
+// exp + log1p per element (the pass was bound by that arithmetic: cfg5 7.0 ms for 8.2 GB).  Any other
+// logit or label computes the term.
+constexpr int kBceGrid = 64;  // table covers x = k/2, |k| <= kBceGrid
+__device__ __forceinline__ float bce_term_tab(float x, float t, const float (*tab)[2 * kBceGrid + 1]) {
+    const float k2 = x * 2.f;  // exact
+    if (k2 == rintf(k2) && fabsf(k2) <= (float)kBceGrid && (t == 0.f || t == 1.f))
+        return tab[t == 1.f][(int)k2 + kBceGrid];
+    return bce_term(x, t);
+}
+
 __global__ __launch_bounds__(256) void bce_loss_kernel(BceArgs a, const float* __restrict__ target, int64_t n,
                                                        double* __restrict__ part) {
     __shared__ double red[4];
+    __shared__ float tab[2][2 * kBceGrid + 1];
+    for (int i = threadIdx.x; i < 2 * (2 * kBceGrid + 1); i += blockDim.x) {
+        const int lab = i / (2 * kBceGrid + 1), k = i % (2 * kBceGrid + 1) - kBceGrid;
+        tab[lab][k + kBceGrid] = bce_term(0.5f * (float)k, (float)lab);
+    }
+    __syncthreads();
+#define bce_term(x, t) bce_term_tab((x), (t), tab)
     double acc0 = 0.0, acc1 = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -156,6 +176,7 @@ __global__ __launch_bounds__(256) void bce_loss_kernel(BceArgs a, const float* _
         const float t = target ? target[i] : 0.f;
         for (int k = 0; k < a.K; ++k) acc0 += (double)a.coef[k] * (double)bce_term(a.x[k][i], t);
     }
+#undef bce_term
     double acc = acc0 + acc1;
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;

@@ -245,3 +245,26 @@ def test_bce_multi_matches_torch(K, etha):
     for o, r in zip(outs, ref_outs):
         np.testing.assert_allclose(o.grad.cpu().numpy(), r.grad.cpu().numpy(), rtol=1e-5,
                                    atol=1e-6 * r.grad.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_bce_loss_grid_table_path():
+    """The loss pass takes half-integer logits with 0/1 labels (every QMS decoder output) from a table of
+    the same term function (nldpc_aux.hip bce_term_tab): grid logits, off-grid logits, logits past the
+    table's range and a non-binary label, one call, against the fp64 reference and its derived bound;
+    and a grid-only call must equal the direct formula's fp64 sum of torch's terms within the bound."""
+    from boosted_neural_ldpc_decoder.LDPCDecoderLoss import LDPCDecoderLoss
+    from boosted_neural_ldpc_decoder.struct.LossType import LossType
+    g = torch.Generator().manual_seed(5)
+    n0, n1, K = 64, 1999, 9
+    grid = [torch.randint(-80, 81, (n0, n1), generator=g).float() * 0.5 for _ in range(K)]  # |k| up to 80 > 64
+    mixed = [x.clone() for x in grid]
+    for x in mixed[::2]:
+        x[::3] += 0.123  # off the grid
+    for y in ((torch.rand(n0, n1, generator=g) < 0.5).float(),
+              torch.where(torch.rand(n0, n1, generator=g) < 0.1, torch.tensor(0.3), torch.tensor(1.0))):
+        for outs in (grid, mixed):
+            dev_outs = [o.to(DEV) for o in outs]
+            loss = LDPCDecoderLoss(loss_type=LossType.BCE, etha=1.0)(dev_outs, y.to(DEV), coeff_param=list(range(K)))
+            ref64, bound, _ = bce_reference(outs, y)
+            assert_loss(loss.item(), ref64, bound)

@@ -31,6 +31,18 @@ for s in $PHASES; do
            (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof_cfg2 -o run --output-format csv \
                -- python3 $R/bench.py --workload cfg2 --steps 500 --warmup 20 --no-cpu-baseline --no-profile --no-count-only > $O/${TAG}_bench_cfg2_under_rocprof.log 2>&1); rc=$?
            tail -c 400 $O/${TAG}_bench_cfg2_noprof.log ;;
+    valumix) (cd /tmp && timeout -s KILL 120 rocprofv3 -L > $O/${TAG}_counters_list.txt 2>&1; \
+             timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_SALU SQ_INSTS_LDS \
+               --kernel-trace -d $O/${TAG}_valumix -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --batch 16384 --no-cpu-baseline --no-profile --no-sweep --no-count-only > $O/${TAG}_valumix.log 2>&1); rc=$?
+           python3 tools/sq_summary.py $O/${TAG}_valumix | grep -A9 "kernel<3" ;;
+    stampsucn) NLDPC_LIB_PATH=$R/neural-ldpc-decoder-torch_amd/lib_stamps/libnldpc.so NLDPC_STAMPS=$O/${TAG}_stamps_ucn.bin \
+             timeout -k 10 300 python -u bench.py --workload cfg3ucn --steps 1 --warmup 1 --batch 16384 --no-profile --no-cpu-baseline > $O/${TAG}_stamps_ucn_bench.log 2>&1 &&
+           python3 tools/stamps2.py $O/${TAG}_stamps_ucn.bin > $O/${TAG}_stamps_ucn.txt 2>&1; rc=$?; head -30 $O/${TAG}_stamps_ucn.txt ;;
+    abq)   for v in ${VARIANTS}; do
+               NLDPC_LIB_PATH=$R/neural-ldpc-decoder-torch_amd/lib_exp/$v/libnldpc.so timeout -k 10 300 python -u bench.py --workload ${WL:-cfg3ucn} ${BENCH_ARGS} \
+                   --steps ${NSTEPS:-4} --warmup 2 --no-cpu-baseline > $O/${TAG}_abq_$v.log 2>&1 || { echo "$v failed"; tail -5 $O/${TAG}_abq_$v.log; exit 1; }
+               python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d.get('ms_per_step_median'), d.get('roofline',{}).get('per_kernel'))" $O/${TAG}_abq_$v.log $v | cut -c1-400
+           done; rc=0 ;;
     *) echo "unknown step $s"; rc=2 ;;
     esac
     echo "== $s rc=$rc"
