@@ -585,7 +585,7 @@ def emit(S: Spec) -> str:
                 for k, e in mine:
                     w(f"    {own_lv(e, q, e0)} = {ref(p, q, k)};")
                     if not SAVECOPY:
-                        w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(p, q, k)}, a.qbit);")
+                        w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(p, q, k)}, a.qp);")
             if d1:  # v2c = (0 + xin) + 0: no other edge in the column (bypass: the check node reads xa)
                 w("    if constexpr (!D1_BYPASS) {")
             for j, e in d1:
@@ -593,7 +593,7 @@ def emit(S: Spec) -> str:
                     v1 = f"fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f)" if ZADD else f"chan<KIND>({xref(p, j, q)}, a)"
                     w(f"    {{ const float v_ = {v1}; "
                       f"{own_lv(e, q, e0)} = v_; " +
-                      ("}" if SAVECOPY else f"if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qbit); }}"))
+                      ("}" if SAVECOPY else f"if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qp); }}"))
             if d1:
                 w("    }")
             w("}")
@@ -812,9 +812,9 @@ def emit(S: Spec) -> str:
         for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
             NE = (e1c - e0c) * Z
             w("template <int KIND>")
-            w(f"__device__ __forceinline__ void save_c{ci}(const float* lds_all, char* svb, int nlive, int qbit) {{")
+            w(f"__device__ __forceinline__ void save_c{ci}(const float* lds_all, char* svb, int nlive, const QParams& qp) {{")
             w("    const int t = threadIdx.x;")
-            w("    (void)qbit;")
+            w("    (void)qp;")
             for g in range(G):
                 src = f"(lds_all + {g * CF * S.nbuf})"
                 w(f"    if ({g} < nlive) {{")
@@ -827,13 +827,13 @@ def emit(S: Spec) -> str:
                     w("#pragma unroll")
                     w("                for (int k = 0; k < 4; ++k) {")
                     w("                    const float4 v = s4[k];")
-                    w("                    o[k] = ((uint32_t)qms_code(v.x, qbit) & 255u) | (((uint32_t)qms_code(v.y, qbit) & 255u) << 8) |")
-                    w("                           (((uint32_t)qms_code(v.z, qbit) & 255u) << 16) | ((uint32_t)qms_code(v.w, qbit) << 24);")
+                    w("                    o[k] = ((uint32_t)qms_code_p(v.x, qp) & 255u) | (((uint32_t)qms_code_p(v.y, qp) & 255u) << 8) |")
+                    w("                           (((uint32_t)qms_code_p(v.z, qp) & 255u) << 16) | ((uint32_t)qms_code_p(v.w, qp) << 24);")
                     w("                }")
                     w("                reinterpret_cast<uint4*>(dst)[i] = make_uint4(o[0], o[1], o[2], o[3]);")
                     w("            }")
                 else:
-                    w(f"            for (int i = t; i < {NE}; i += {S.threads}) dst[i] = (int8_t)qms_code({src}[i], qbit);")
+                    w(f"            for (int i = t; i < {NE}; i += {S.threads}) dst[i] = (int8_t)qms_code_p({src}[i], qp);")
                 w("        } else {")
                 w(f"            float* dst = (float*)(svb + {4 * (g * S.E + e0c) * Z});")
                 if NE % 4 == 0 and (g * CF * S.nbuf) % 4 == 0:
@@ -1021,7 +1021,7 @@ def emit(S: Spec) -> str:
                 stamp(2 + 3 * ci)
                 w("        __syncthreads();")
                 if SAVECOPY:  # the image holds the chunk's v2c: save it before the check nodes overwrite it
-                    w(f"        if constexpr (SAVE) {{ if (svb) save_c{ci}<KIND>(lds_all, svb, nlive, a.qbit); __syncthreads(); }}")
+                    w(f"        if constexpr (SAVE) {{ if (svb) save_c{ci}<KIND>(lds_all, svb, nlive, a.qp); __syncthreads(); }}")
                 op_cn(ci)
                 stamp(3 + 3 * ci)
                 w("        __syncthreads();")

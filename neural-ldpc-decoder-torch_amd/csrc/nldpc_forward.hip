@@ -280,8 +280,10 @@ static bool fused_eligible(const nldpc_graph* g, const nldpc_cfg* cfg, int32_t T
     const bool saving = mode == 1;
     static const bool disabled = std::getenv("NLDPC_DISABLE_FUSED") != nullptr;
     if (disabled || (cfg->flags & NLDPC_FLAG_STREAM)) return false;
-    // the SAVE kernels write what the backward needs (QMS: int8 codes, which need an active quantiser)
-    if (saving && cfg->kind == NLDPC_QMS && !qms_active(cfg->qbit)) return false;
+    // QMS: the fused kernels' check node is the active quantiser's (boosted_row), and the SAVE kernels'
+    // int8 codes need one too; an inactive qbit decodes on the streaming kernels
+    (void)saving;
+    if (cfg->kind == NLDPC_QMS && !qms_active(cfg->qbit)) return false;
     return fused_launch(g, mode, cfg->kind) && !cfg->c2v_in && T <= kFusedMaxT;
 }
 
@@ -296,6 +298,7 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     fa.B = B;
     fa.T = T;
     fa.qbit = cfg->qbit;
+    fa.qp = q_params(cfg->qbit);
     fa.xa = xa;
     fa.w_cn = w_cn;
     fa.bias = bias;

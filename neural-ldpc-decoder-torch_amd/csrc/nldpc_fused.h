@@ -18,6 +18,7 @@ struct FusedArgs {
     int64_t B;
     int32_t T;
     int32_t qbit;
+    QParams qp;          // QMS: the active quantiser's constants (q_params(qbit)); QMS needs an active q here
     const float* xa;     // [B][N][Z]
     const float* w_cn;   // [T][E] or nullptr
     const float* bias;   // [T][E] or nullptr
@@ -82,17 +83,17 @@ constexpr int saved_msg_bytes() { return KIND == NLDPC_QMS ? 1 : 4; }
 // QMS quantiser of the channel values and posteriors in the fused kernels
 // (the generic quantize(): the four-operation quantize_active behind a select measured 15 % slower in the
 // fused QMS kernels, cfg3 NW(1,1,2) 187.6 -> 217 ms -- register allocation, not operation count)
-__device__ __forceinline__ float qms_q(float x, int q) { return quantize(x, q); }
+__device__ __forceinline__ float qms_q(float x, const QParams& p) { return quantize_p(x, p); }
 
 template <int KIND>
 __device__ __forceinline__ float chan(float x, const FusedArgs& a) {
     if (KIND == NLDPC_NEURAL || a.w_vn) return x;
-    return KIND == NLDPC_QMS ? qms_q(x, a.qbit) : x;
+    return KIND == NLDPC_QMS ? qms_q(x, a.qp) : x;
 }
 template <int KIND>
 __device__ __forceinline__ float chan_step(float x, const FusedArgs& a, float w) {
     x = fmul(x, w);
-    return KIND == NLDPC_QMS ? qms_q(x, a.qbit) : x;
+    return KIND == NLDPC_QMS ? qms_q(x, a.qp) : x;
 }
 
 // posterior of one variable copy: Neural xa + P; Boosted clamp(Q(xa) + P) (Boosted…py:513-521), the
@@ -100,7 +101,7 @@ __device__ __forceinline__ float chan_step(float x, const FusedArgs& a, float w)
 template <int KIND>
 __device__ __forceinline__ float posterior(float xav, float P, const FusedArgs& a) {
     if (KIND == NLDPC_NEURAL) return fadd(xav, P);
-    const float xo = (KIND == NLDPC_QMS) ? qms_q(xav, a.qbit) : xav;
+    const float xo = (KIND == NLDPC_QMS) ? qms_q(xav, a.qp) : xav;
     return __builtin_amdgcn_fmed3f(fadd(xo, P), a.lo, a.hi);
 }
 
@@ -116,15 +117,15 @@ __device__ __forceinline__ f2 posterior2(f2 xav, f2 P, const FusedArgs& a) {
 
 // one saved v2c message (training forward): fp32, or the QMS int8 code (byte offset = float offset / 4)
 template <int KIND>
-__device__ __forceinline__ void save_v2c(rsrc_t r, uint32_t vc, int elem, float v, int qbit) {
-    if constexpr (KIND == NLDPC_QMS) bstore_i8(r, vc >> 2, elem, qms_code(v, qbit));
+__device__ __forceinline__ void save_v2c(rsrc_t r, uint32_t vc, int elem, float v, const QParams& qp) {
+    if constexpr (KIND == NLDPC_QMS) bstore_i8(r, vc >> 2, elem, qms_code_p(v, qp));
     else bstore(r, vc, 4 * elem, v);
 }
 
 // Boosted posterior and its clamp mask (saved for the backward): in_range of the pre-clamp value
 template <int KIND>
 __device__ __forceinline__ float posterior_m(float xav, float P, const FusedArgs& a, bool& m) {
-    const float xo = (KIND == NLDPC_QMS) ? qms_q(xav, a.qbit) : xav;
+    const float xo = (KIND == NLDPC_QMS) ? qms_q(xav, a.qp) : xav;
     const float yp = fadd(xo, P);
     m = yp >= a.lo && yp <= a.hi;
     return clampf(yp, a.lo, a.hi);
@@ -641,7 +642,7 @@ __device__ __forceinline__ void PostSink::flush_wave(int* cntl, int it) {
 // as one sign select.  Results equal cn_core + cn_epilogue (a zero c2v may differ in its sign bit
 // only, which no sum of the decoder can observe).  ~19 VALU per edge copy instead of ~45.
 template <int DC, int KIND>
-__device__ __forceinline__ void boosted_row_keys(float (&m)[DC], const float (&w)[DC], bool has_w, int qbit, float lo,
+__device__ __forceinline__ void boosted_row_keys(float (&m)[DC], const float (&w)[DC], bool has_w, const QParams& qp, float lo,
                                                  float hi, bool ucn, float uf, const float (&wu)[DC]) {
     constexpr uint32_t kInit = 0x461C4000u << 1;  // key of 10000.f
     uint32_t key[DC];
@@ -649,7 +650,7 @@ __device__ __forceinline__ void boosted_row_keys(float (&m)[DC], const float (&w
     bool par = false;
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        float x = KIND == NLDPC_QMS ? quantize_active(m[k], qbit) : __builtin_amdgcn_fmed3f(m[k], lo, hi);
+        float x = KIND == NLDPC_QMS ? quantize_active_p(m[k], qp) : __builtin_amdgcn_fmed3f(m[k], lo, hi);
         x = x == 0.f ? kZeroFix : x;
         key[k] = __builtin_bit_cast(uint32_t, x) << 1;
         pos[k] = x > 0.f;
@@ -682,7 +683,7 @@ __device__ __forceinline__ void boosted_row_keys(float (&m)[DC], const float (&w
                          : (ucn ? fadd(fmul(fmul(mag, w[k]), fadd(-uf, 1.f)), fmul(fmul(mag, wu[k]), uf))
                                 : fmul(mag, w[k]));
         const float x2 = relu_mask(x1);
-        const float x3 = KIND == NLDPC_QMS ? quantize_active(x2, qbit) : __builtin_amdgcn_fmed3f(x2, lo, hi);
+        const float x3 = KIND == NLDPC_QMS ? quantize_active_p(x2, qp) : __builtin_amdgcn_fmed3f(x2, lo, hi);
         const bool neg = KIND == NLDPC_MS && (sel ? n2 : n1);
         m[k] = ((par != pos[k]) != neg) ? x3 : -x3;
     }
@@ -705,7 +706,7 @@ __device__ __forceinline__ void boosted_row_keys(float (&m)[DC], const float (&w
 // (the masked 10000 would be the magnitude) keep the key form.  Equal to boosted_row_keys up to the
 // sign bit of a zero c2v, which no sum of the decoder observes.
 template <int DC, int KIND>
-__device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC], bool has_w, int qbit, float lo,
+__device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC], bool has_w, const QParams& qp, float lo,
                                             float hi, bool ucn, float uf, const float (&wu)[DC]) {
     if constexpr (DC >= 2) {
         float min1, min2;
@@ -723,9 +724,9 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
                 top = hi;
                 inv = 1.f;
             } else {
-                const float s = qbit == 5 ? 2.f : (qbit == 3 ? 0.5f : 1.f);
-                inv = qbit == 5 ? 0.5f : (qbit == 3 ? 2.f : 1.f);
-                top = qbit == 6 ? 15.5f : (qbit == 5 ? 15.f : (qbit == -5 ? 15.f : (qbit == 4 ? 7.f : 3.f)));  // hi * s
+                const float s = qp.s;
+                inv = qp.inv;
+                top = qp.hs;  // hi * s
                 // s * Q(min) = min(rint(min s), hi s): the magnitude pre-scaled by s, so the per-edge
                 // product (s mag) w = s (mag w) exactly and Q's own scaling needs no multiply
                 mg1 = fminf(rintf(fmul(min1, s)), top);
@@ -755,7 +756,7 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
             return;
         }
     }
-    boosted_row_keys<DC, KIND>(m, w, has_w, qbit, lo, hi, ucn, uf, wu);
+    boosted_row_keys<DC, KIND>(m, w, has_w, qp, lo, hi, ucn, uf, wu);
 }
 
 // check node of one check copy in place (m: gathered v2c -> c2v), every kind: Neural through the
@@ -766,8 +767,10 @@ __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], c
                                         const FusedArgs& a, bool has_w, int row, float uf) {
     if constexpr (KIND == NLDPC_NEURAL) {
         neural_row<DC>(m, wv, bv);
-    } else if (KIND == NLDPC_MS || (KIND == NLDPC_QMS && qms_active_q(a.qbit))) {
-        boosted_row<DC, KIND>(m, wv, has_w, a.qbit, a.lo, a.hi, a.ucn != 0, uf, bv);
+    } else if constexpr (KIND == NLDPC_MS || KIND == NLDPC_QMS) {
+        // QMS reaches the fused kernels only with an active quantiser (fused_eligible): the generic
+        // cn_core is not compiled into them (it had made the QMS kernels 6x the code of the MS ones)
+        boosted_row<DC, KIND>(m, wv, has_w, a.qp, a.lo, a.hi, a.ucn != 0, uf, bv);
     } else {
         CnCore<DC> core;
         cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core, SpRow{a.sp_plan + row * kSpPlanBytes, a.tanh});

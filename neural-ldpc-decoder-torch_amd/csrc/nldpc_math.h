@@ -73,6 +73,28 @@ __device__ __forceinline__ float quantize_active(float x, int q) {
 }
 __device__ __forceinline__ bool qms_active_q(int q) { return q == 6 || q == 5 || q == -5 || q == 4 || q == 3; }
 
+// An active quantiser's constants, computed once on the host (FusedArgs::qp) so the fused kernels read
+// four kernel-argument floats instead of re-deriving them from q with scalar compare/select chains at
+// every use: scale s, 1/s, clip hi and hi*s (s in {2, 1, 1/2}: every scaling is exact).
+struct QParams {
+    float s, inv, hi, hs;
+};
+__host__ __device__ inline QParams q_params(int q) {
+    const float s = q == 5 ? 2.f : (q == 3 ? 0.5f : 1.f);
+    const float hi = q == 6 ? 15.5f : (q == 5 ? 7.5f : (q == -5 ? 15.f : (q == 4 ? 7.f : 6.f)));
+    return QParams{s, q == 5 ? 0.5f : (q == 3 ? 2.f : 1.f), hi, hi * s};
+}
+// quantize() for an active q (the reference's STE form, same operations in the same order)
+__device__ __forceinline__ float quantize_p(float x, const QParams& p) {
+    const float qv = clampf(fmul(rintf(fmul(x, p.s)), p.inv), -p.hi, p.hi);
+    const float xc = clampf(x, -p.hi, p.hi);
+    return fadd(xc, __fsub_rn(qv, xc));
+}
+// quantize_active() with the constants given
+__device__ __forceinline__ float quantize_active_p(float x, const QParams& p) {
+    return fmul(__builtin_amdgcn_fmed3f(rintf(fmul(x, p.s)), -p.hs, p.hs), p.inv);
+}
+
 // QMS training state.  The backward reads a saved v2c message m only through Q(m) and the STE mask of
 // Q's clip on m, so QMS saves one signed byte 2*m' per message: m' = Q(m) inside the clip range and
 // sign(m) * (hi + 1) outside it, which gives Q(m') == Q(m) and the same mask (Q's values are
@@ -93,6 +115,13 @@ __device__ __forceinline__ int qms_code(float m, int q) {
     const float c_out = 2.f * r.hi + 2.f;
     const float t = fmul(__builtin_amdgcn_fmed3f(rintf(fmul(m, s)), -hs, hs), k2);
     const float c = fabsf(m) <= r.hi ? t : (m > 0.f ? c_out : -c_out);
+    return (int)c;
+}
+// qms_code() for an active q with the constants given (2 / s = 2 inv)
+__device__ __forceinline__ int qms_code_p(float m, const QParams& p) {
+    const float c_out = 2.f * p.hi + 2.f;
+    const float t = fmul(__builtin_amdgcn_fmed3f(rintf(fmul(m, p.s)), -p.hs, p.hs), 2.f * p.inv);
+    const float c = fabsf(m) <= p.hi ? t : (m > 0.f ? c_out : -c_out);
     return (int)c;
 }
 __device__ __forceinline__ float qms_decode(int c) { return 0.5f * (float)c; }

@@ -43,6 +43,10 @@ for s in $PHASES; do
                    --steps ${NSTEPS:-4} --warmup 2 --no-cpu-baseline > $O/${TAG}_abq_$v.log 2>&1 || { echo "$v failed"; tail -5 $O/${TAG}_abq_$v.log; exit 1; }
                python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d.get('ms_per_step_median'), d.get('roofline',{}).get('per_kernel'))" $O/${TAG}_abq_$v.log $v | cut -c1-400
            done; rc=0 ;;
+    stamps5) NLDPC_LIB_PATH=$R/neural-ldpc-decoder-torch_amd/lib_stamps/libnldpc.so NLDPC_STAMPS=$O/${TAG}_stamps5_fwd.bin NLDPC_STAMPS_BWD=$O/${TAG}_stamps5_bwd.bin \
+             timeout -k 10 300 python -u bench.py --workload cfg5 --steps 1 --warmup 0 --batch 512 --no-profile --no-cpu-baseline > $O/${TAG}_stamps5_bench.log 2>&1 &&
+           python3 tools/stamps2.py $O/${TAG}_stamps5_fwd.bin > $O/${TAG}_stamps5_fwd.txt 2>&1 && python3 tools/stamps_bwd.py $O/${TAG}_stamps5_bwd.bin ${KB:-3} > $O/${TAG}_stamps5_bwd.txt 2>&1; rc=$?
+           head -14 $O/${TAG}_stamps5_fwd.txt; head -20 $O/${TAG}_stamps5_bwd.txt ;;
     *) echo "unknown step $s"; rc=2 ;;
     esac
     echo "== $s rc=$rc"
