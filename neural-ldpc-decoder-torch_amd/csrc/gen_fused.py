@@ -124,6 +124,10 @@ GWQ = os.environ.get("NLDPC_GEN_GWQ", "1") == "1"
 # profiles/r3b_ab.txt; register allocation), though they are ~2 % of the VALU instructions
 ZADD = os.environ.get("NLDPC_GEN_ZADD", "1") == "1"
 
+# the wave UCN in the QMS kernels too (r2 measured it slower there, 180 -> 217 ms, before the QMS kernels lost
+# their generic check node in r3)
+UCNW_QMS = os.environ.get("NLDPC_GEN_UCNW_QMS", "0") == "1"
+
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
 
@@ -329,7 +333,8 @@ def emit(S: Spec) -> str:
     w("#define D1_BYPASS (KIND == NLDPC_NEURAL && !SAVE)")
     w("// check-row LDS addresses from one 32-bit base (ROADDR); in the QMS / SP kernels it measured slower")
     w("#define ROA (KIND == NLDPC_NEURAL || KIND == NLDPC_MS)")
-    w(f"#define UCNW (KIND == NLDPC_MS && {'true' if S.ucn_wave else 'false'})  // UCN bits by waves (Spec.ucn_wave)")
+    w(f"#define UCNW ((KIND == NLDPC_MS{' || KIND == NLDPC_QMS' if UCNW_QMS else ''}) && {'true' if S.ucn_wave else 'false'})  "
+      "// UCN bits by waves (Spec.ucn_wave)")
     assert NZ < 65536  # per-codeword error counts are packed two to an LDS word
 
     # Register state of part p: copies are paired (q = 0,1 / 2,3 ...) into float2 arrays so the VN's
