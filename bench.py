@@ -169,6 +169,14 @@ def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings,
             r["valu_issue"] = {"insts_per_launch": pmc["valu_insts"], "frac_of_peak": round(busy, 4),
                                "peak_insts_per_s": PEAK_VALU_INSTS,
                                "note": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x launch time)"}
+            mix = pmc.get("valu_mix")
+            if mix:  # the same instructions priced at their measured per-class issue cost
+                cyc = sum(mix["fractions"][c] * mix["issue_cycles"][c] for c in mix["fractions"])
+                clk = (pmc.get("effective_clock_ghz") or 2.4) * 1e9
+                r["valu_issue"]["weighted_frac_of_simd_cycles"] = round(
+                    pmc["valu_insts"] * cyc / (1024 * clk * d["avg_ms"] / 1000.0), 4)
+                r["valu_issue"]["weighted_note"] = ("instructions x mean issue cycles of the kernel's PMC class mix / "
+                                                    "(1024 SIMDs x effective clock x launch time): pmc.valu_mix")
     if dom == "fused" and d5_bytes_per_cw:
         # SURVEY §8(d) D5 models a flooding decoder whose E*Z message state crosses HBM every iteration;
         # the fused kernel keeps that state on chip, so this is an equivalent rate, not traffic

@@ -22,7 +22,7 @@ for s in $PHASES; do
                -- python3 $R/bench.py --workload cfg5 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_cfg5_under_rocprof.log 2>&1); rc=$? ;;
     cfg2)  timeout -k 10 300 python -u bench.py --workload cfg2 --steps 50 --warmup 5 --no-cpu-baseline > $O/${TAG}_bench_cfg2.log 2>&1; rc=$?; tail -c 800 $O/${TAG}_bench_cfg2.log ;;
     ucn)   timeout -k 10 600 python -u bench.py --workload cfg3ucn --steps 5 --warmup 2 --no-cpu-baseline > $O/${TAG}_bench_ucn_MS_112.log 2>&1 &&
-           timeout -k 10 600 python -u bench.py --workload cfg3ucn --kind QMS --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_ucn_QMS_112.log 2>&1; rc=$?
+           timeout -k 10 600 python -u bench.py --workload cfg3ucn --kind QMS --steps 3 --warmup 2 --no-cpu-baseline > $O/${TAG}_bench_ucn_QMS_112.log 2>&1; rc=$?
            tail -c 600 $O/${TAG}_bench_ucn_MS_112.log; tail -c 600 $O/${TAG}_bench_ucn_QMS_112.log ;;
     ab)    VARIANTS="${VARIANTS}" STEPS=6 bash tools/gpu_ab.sh > $O/${TAG}_ab.txt 2>&1; rc=$?; cat $O/${TAG}_ab.txt ;;
     icache) bash tools/gpu_icache.sh > $O/${TAG}_icache.txt 2>&1; rc=$?; cat $O/${TAG}_icache.txt ;;

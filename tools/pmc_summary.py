@@ -5,7 +5,9 @@ FETCH_SIZE / WRITE_SIZE are in KiB.  Calibration on the probe kernels with known
 (tools/probe_pmc.py, 1 GiB each): WRITE_SIZE reads the written bytes exactly; FETCH_SIZE reports half
 the bytes of a coalesced streaming read at both 16 B and 4 B per lane (the decoder's width), so fetch
 bytes = 2 x FETCH_SIZE x 1024 (MI355X_MICROARCH.md, HBM/rocprofv3 section).
-Usage: python tools/pmc_summary.py gpurun_out r2 > profiles/pmc_traffic.json"""
+Usage: python tools/pmc_summary.py gpurun_out r2 [previous.json] > profiles/pmc_traffic.json (entries of
+workloads not re-measured are kept from previous.json).  (The QMS backward's namespace is fusedbq_ since r2:
+the kernel is matched by its suffix.)"""
 import collections
 import csv
 import json
@@ -42,7 +44,7 @@ out["calibration"] = {
     "fetch_ratio_16B": fv[2] * 1024 / gib, "fetch_ratio_4B": fv[3] * 1024 / gib, "write_ratio": wv[1] * 1024 / gib,
 }
 KERNELS = {"cfg3": [("fused", "fused_bg2_z384::kernel<3, 0>", 65536)],
-           "cfg5": [("fused", "fused_bg2_z384::kernel<2, 1>", 2048), ("fusedb", "fusedb_bg2_z384::bwd_kernel<2>", 2048)],
+           "cfg5": [("fused", "fused_bg2_z384::kernel<2, 1>", 2048), ("fusedb", "_bg2_z384::bwd_kernel<2>", 2048)],
            "cfg3ucn": [("fused", "fused_bg2_z384::kernel<1, 0>", 65536)]}
 for w, ks in KERNELS.items():
     if not os.path.isdir(os.path.join(root, f"{tag}_{w}_sq")):
@@ -65,5 +67,8 @@ for w, ks in KERNELS.items():
                "effective_clock_ghz": (c["GRBM_GUI_ACTIVE"] / 8 / (d * 1e6)) if c.get("GRBM_GUI_ACTIVE") and d else None,
                "source": f"gpurun_out/{tag}_{w}_{{fetch,write,sq}} (rocprofv3 --pmc, one group per run)"}
         out[f"{short}_{w}_B{B}"] = rec
+if len(sys.argv) > 3:  # keep the workloads this tag did not measure
+    for k, v in json.load(open(sys.argv[3])).items():
+        out.setdefault(k, v)
 json.dump(out, sys.stdout, indent=1)
 print()
