@@ -97,8 +97,9 @@ int nldpc_graph_kernels(const nldpc_graph* g, uint32_t* mask);
 /* ---- execution path.  *eligible = 1 when nldpc_forward with these arguments runs the fused
  *      register-resident kernel: a (base graph, lifting size) compiled in, no incoming message state
  *      (c2v_in == 0; a resumed UCN segment passes app_prev instead), T <= 64, no NLDPC_FLAG_STREAM;
- *      every kind, UCN and cumulative VN weights included, and saving for backward included except
- *      QMS with an identity quantiser.  Then v2c is unused, and c2v is unused too with
+ *      every kind, UCN and cumulative VN weights included, saving for backward included; QMS only
+ *      with an active quantiser (qbit 3, 4, 5, -5, 6: an identity quantiser decodes on the streaming
+ *      kernels, r3).  Then v2c is unused, and c2v is unused too with
  *      NLDPC_FLAG_NO_STATE.  Otherwise the streaming kernels run and need both buffers. */
 int nldpc_fast_path(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, int32_t T, int32_t saving,
                     int32_t* eligible);

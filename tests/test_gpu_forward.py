@@ -470,3 +470,33 @@ def test_runtime_kernel_training_step_matches_streaming():
     for k in (1, 2):
         a, b = res["stream"][k].cpu().numpy(), res["fused"][k].cpu().numpy()
         np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-5 * np.abs(a).max())
+
+
+@pytest.mark.parametrize("q", [0, 2])
+def test_qms_inactive_quantiser_runs_on_streaming_path(q):
+    """QMS with a qbit the reference's quantiser does not know (Boosted…py:187-214: the message passes
+    unquantised) has no fused kernel (the fused QMS kernels carry only the active quantiser's check
+    node): nldpc_fast_path reports 0, path="fused" is refused, and the default path
+    decodes on the streaming kernels, bit-exact against the CPU oracle."""
+    import ctypes
+    from nldpc import _lib
+    from nldpc.decode import DecodeCfg, decode
+    from oracle.ldpc_oracle import OracleGraph, boosted_forward
+    L = _lib.lib()
+    T, B, Z = 5, 3, 16
+    g = _graph(BG2, Z)
+    for save in (0, 1):
+        cfg = DecodeCfg(2, qbit=q).c_struct(False)
+        out = ctypes.c_int32(-1)
+        _lib.check(L.nldpc_fast_path(g.handle(DEV), ctypes.byref(cfg), B, T, save, ctypes.byref(out)))
+        assert out.value == 0, (q, save)
+    gen = torch.Generator().manual_seed(40 + q)
+    x = (2 * (-1 + 0.9 * torch.randn(B, 52, Z, generator=gen)) / 0.81).float()
+    w_cn = (0.75 + 0.5 * torch.rand(T, g.E, generator=gen))
+    with pytest.raises(_lib.NldpcError):
+        decode(g, DecodeCfg(2, qbit=q, path="fused"), x.to(DEV), T, w_cn=w_cn.to(DEV))
+    outs, _, _ = decode(g, DecodeCfg(2, qbit=q), x.to(DEV), T, w_cn=w_cn.to(DEV))
+    ref = boosted_forward(OracleGraph(BG2, Z), x, dtype=2, q=q, nw=(1, 0, 0), iters=list(range(T)),
+                          w_cn=lambda t: w_cn[t], w_ucn=lambda t: None, w_vn=lambda t: None)
+    for t in range(T):
+        assert torch.equal(outs[t].cpu(), ref[t]), f"iteration {t}"
