@@ -128,6 +128,9 @@ ZADD = os.environ.get("NLDPC_GEN_ZADD", "1") == "1"
 # their generic check node in r3)
 UCNW_QMS = os.environ.get("NLDPC_GEN_UCNW_QMS", "0") == "1"
 
+# experiment knob: CN work units balanced together with the owner LDS traffic of the same barrier interval
+CNBAL_ALPHA = float(os.environ.get("NLDPC_GEN_CNBAL_ALPHA", "0"))
+
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
 
@@ -295,10 +298,22 @@ class Spec:
         # 18, 12, 0; by units at most 21).  NLDPC_GEN_CNUNIT=0: whole rows (cn_rows)
         if CNUNIT:
             self.cn_units = []
-            for r0, r1, _, _ in self.chunks:
+            K = len(self.chunks)
+
+            def owner_msgs(p, c):  # register messages part p writes / reads back for chunk c
+                if c < 0 or c >= K:
+                    return 0
+                e0, e1 = self.chunks[c][2], self.chunks[c][3]
+                return Q * sum(1 for e in self.slots[p] if e0 <= e < e1)
+            for ci, (r0, r1, _, _) in enumerate(self.chunks):
                 units = sorted(((i, q) for i in range(r0, r1) for q in range(Q)),
                                key=lambda iq: (-len(self.row_edges[iq[0]]), iq[0], iq[1]))
-                load, bins = [0] * P, [[] for _ in range(P)]
+                # CNBAL_ALPHA > 0 (pipelined schedule): start each part's load at the owner LDS traffic it
+                # runs in the same barrier interval (CN_c with W_{c+1} for even c, with R_{c-1} for odd c),
+                # priced at alpha check-node edge copies per message
+                partner = (ci + 1) if ci % 2 == 0 else (ci - 1)
+                load = [CNBAL_ALPHA * owner_msgs(p_, partner) if pipe else 0 for p_ in range(P)]
+                bins = [[] for _ in range(P)]
                 for i, q in units:
                     k = int(np.argmin(load))
                     bins[k].append((i, q))
