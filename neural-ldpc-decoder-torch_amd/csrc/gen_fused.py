@@ -229,7 +229,9 @@ class Spec:
         # its columns' vectors XOR-ed once per row and wave, not gathered bit by bit per copy and edge.
         # (used by the MS kernels only: in the QMS kernels the extra scalar state measured slower, 180 -> 217 ms
         # at cfg3 NW(1,1,2), register allocation; UCNW in the generated code)
-        self.ucn_wave = self.ZT % 64 == 0 and Z % 32 == 0 and os.environ.get("NLDPC_GEN_UCNWAVE", "1") == "1"
+        # r3: off by default -- after the r3 kernel changes the per-copy form is faster for MS too (cfg3 MS
+        # NW(1,1,2) + UCN kernel 111.6 -> 107.6 ms, same-box A/B, profiles/r3t_ab_ms_ucnw.txt)
+        self.ucn_wave = self.ZT % 64 == 0 and Z % 32 == 0 and os.environ.get("NLDPC_GEN_UCNWAVE", "0") == "1"
         self.lanes = G * self.ZT  # live threads per part
         # A part occupies whole waves.  The lanes past the live ones (padded parts) run the code of the
         # first live lanes (same copies) on an LDS region of their own and with global offsets out of
