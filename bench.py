@@ -136,6 +136,14 @@ def load_pmc(key):
     return v if isinstance(v, dict) else None
 
 
+def pmc_workload(args):
+    """The key of this run's counters in profiles/pmc_traffic.json: the Boosted side lines are keyed by
+    decoding type and sharing codes (their kernels differ), e.g. cfg3ucn_QMS_NW112."""
+    if args.workload == "cfg3ucn":
+        return f"cfg3ucn_{args.kind}_NW{args.nw.replace(',', '')}"
+    return args.workload
+
+
 def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings, pmc_key):
     """Roofline of the dominant kernel: the algorithmic bytes it must move per launch over its average
     HIP-event launch time, against the 8 TB/s HBM spec (and the measured HBM ceilings); HBM traffic
@@ -404,7 +412,7 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
                                                     "frame_errors_last_iter": lit_frames[-1], "frames": B}
     if prof is not None:
         res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T), args.steps, B, Z, world, tag,
-                                   4 * (2 * T * E * Z + (T + 1) * N * Z), ceilings, f"{args.workload}_B{B}")
+                                   4 * (2 * T * E * Z + (T + 1) * N * Z), ceilings, pmc_workload(args) + f"_B{B}")
     if world == 1 and not args.no_cpu_baseline and not ucn:
         res["cpu_baseline"] = cpu_baseline(bg, Z, T, xa_host, gpu_last, args.cpu_seconds)
     return res

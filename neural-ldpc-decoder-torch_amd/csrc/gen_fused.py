@@ -131,6 +131,11 @@ UCNW_QMS = os.environ.get("NLDPC_GEN_UCNW_QMS", "0") == "1"
 # experiment knob: CN work units balanced together with the owner LDS traffic of the same barrier interval
 CNBAL_ALPHA = float(os.environ.get("NLDPC_GEN_CNBAL_ALPHA", "0"))
 
+# experiment knob: static wave priority per barrier phase (s_setprio 0-3): within each set of parts that
+# share SIMDs (even / odd parts), the part with the most estimated work in a phase issues first, so the
+# heaviest waves are not left to finish alone at the phase's end (issue is arbitrated by priority, then age)
+PRIO = os.environ.get("NLDPC_GEN_PRIO", "0") == "1"
+
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
 
@@ -876,6 +881,49 @@ def emit(S: Spec) -> str:
     # part's at a control-flow join (per-phase part branches inside one loop made the register
     # allocator insert phi copies and spill).  The parts still meet at every s_barrier: a hardware
     # barrier counts waves, not program counters, and every part executes the same barrier sequence.
+    def pipe_phases(K):
+        # [W0] | [CN0, W1] | [R0, CN1] | [W2, R1] | [CN2, W3] | [R2, CN3] | ... (see the pipelined schedule below)
+        phases = [[("w", 0)]]
+        c = 0
+        while c < K:
+            phases.append([("cn", c)] + ([("w", c + 1)] if c + 1 < K else []))
+            phases.append([("r", c)] + ([("cn", c + 1)] if c + 1 < K else []))
+            if c + 1 < K:
+                phases.append(([("w", c + 2)] if c + 2 < K else []) + [("r", c + 1)])
+            c += 2
+        return phases
+
+    prio = {}
+    if PRIO and S.pipe:
+        # estimated issue cycles per phase and part: VN adds 2, a check-node edge copy ~34 (half-rate
+        # min/select/relu/sign work), an owner LDS message 3 (wrapped copies: compare/select/add)
+        K = len(S.chunks)
+        phases = pipe_phases(K)
+        work = [[0.0] * len(phases) for _ in range(S.P)]
+        for p in range(S.P):
+            vn = sum(len(S.col_edges[j]) * (len(S.col_edges[j]) - 1) // 2 + 2 * len(S.col_edges[j]) + 1
+                     for j in S.reg_cols[p]) * Q
+            work[p][0] += 2 * vn
+            for k, ph in enumerate(phases):
+                for kind_, ci in ph:
+                    e0, e1 = S.chunks[ci][2], S.chunks[ci][3]
+                    if kind_ == "cn":
+                        work[p][k] += 34 * sum(len(S.row_edges[i]) for i, _ in S.cn_units[ci][p])
+                    else:
+                        work[p][k] += 3 * Q * sum(1 for e in S.slots[p] if e0 <= e < e1)
+            if K % 2 == 0:  # the last read-back [R_{K-1}] runs into the next iteration's VN phase
+                work[p][0] += work[p][-1]
+                work[p][-1] = 0
+        for k in range(len(phases)):
+            for par in (0, 1):
+                ps_ = sorted((p for p in range(S.P) if p % 2 == par), key=lambda p: -work[p][k])
+                for r, p in enumerate(ps_):
+                    prio[(p, k)] = max(0, 3 - r)
+
+    def setprio(p, k):
+        if (p, k) in prio:
+            w(f"        __builtin_amdgcn_s_setprio({prio[(p, k)]});")
+
     # this thread's codeword counters (recomputed at each flush: no register held across the iteration)
     cnt_slot = "cntl"  # the kernel passes this codeword's counters
     cnt_flush = "flush_wave" if G == 1 else "flush"  # one codeword per wave: reduce the wave first
@@ -977,6 +1025,7 @@ def emit(S: Spec) -> str:
         w(f"        const rsrc_t pr = make_rsrc(pp ? pp + blk * {NZ} : a.xa, pp ? nlive * {4 * NZ} : 0);  // no output: stores dropped")
         w("        const uint8_t* pmp = (SAVE && a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t pm = make_rsrc((const float*)(pmp ? pmp + blk * {NZ} : nullptr), pmp ? nlive * {NZ} : 0);")
+        setprio(p, 0)
         if "vn" not in SKIP:
             w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
@@ -1054,21 +1103,19 @@ def emit(S: Spec) -> str:
             # phases: [W0] | [CN0, W1] | [R0, CN1] | [W2, R1] | [CN2, W3] | [R2, CN3] | ... | [R_{K-1}] (the last
             # read-back runs into the next iteration's VN and W0, whose buffer was last read two phases back).
             # W_c reuses the buffer of chunk c-2, read (R_{c-2}) a phase earlier.
-            phases = [[("w", 0)]]
-            c = 0
-            while c < K:
-                phases.append([("cn", c)] + ([("w", c + 1)] if c + 1 < K else []))
-                phases.append([("r", c)] + ([("cn", c + 1)] if c + 1 < K else []))
-                if c + 1 < K:
-                    phases.append(([("w", c + 2)] if c + 2 < K else []) + [("r", c + 1)])
-                c += 2
+            phases = pipe_phases(K)
             # phase dependencies hold: each W_c is after R_{c-2}'s phase, each CN_c after W_c's, each R_c after CN_c's
             for k, ph in enumerate(phases):
+                if k > 0 and not (K % 2 == 0 and k == len(phases) - 1):
+                    setprio(p, k)
+                elif k > 0:
+                    setprio(p, 0)  # [R_{K-1}] belongs to the next VN phase
                 for kind_, ci in ph:
                     {"w": op_w, "cn": op_cn, "r": op_r}[kind_](ci)
                 stamp(2 + k)  # arrival at the barrier that ends phase k (stamp 1: after the VN)
                 if k < len(phases) - 1:
-                    w("        __syncthreads();")
+                    # (timing experiment SKIP=sync: no barrier -- racy results, the cost of waiting at them)
+                    w("        __builtin_amdgcn_sched_barrier(0);" if "sync" in SKIP else "        __syncthreads();")
             # a K-odd schedule ends with [R_{K-1}] alone after [R_{K-2}... ]: the next W0 (buffer 0) follows
             # R_{K-1} (buffer 0) in other waves -> keep a barrier; K even: R_{K-1} reads buffer 1
             if K % 2 == 1:

@@ -376,6 +376,9 @@ __device__ __forceinline__ void two_smallest_abs3(const float (&m)[DC], float& m
 #ifndef NLDPC_CN_MAGI
 #define NLDPC_CN_MAGI 0
 #endif
+#ifndef NLDPC_CN_MAGS
+#define NLDPC_CN_MAGS 0
+#endif
 template <int DC>
 __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
     float min1, min2, mg1, mg2;
@@ -415,6 +418,19 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(t) : "v"(ms_), "v"(__float_as_uint(x) & 0x7fffffffu));
         asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(ma_), "v"(mb_), "v"(t));
         return __uint_as_float(r);
+    };
+#elif NLDPC_CN_MAGS
+    // the magnitude select as t = min(|m_k|, mg2) (|m_k| a source modifier) and one integer subtract:
+    // the edge holding the minimum (|m_k| == min1) gets t = mg1 (mg1 = min(min1, cap) <= mg2), every other
+    // edge has |m_k| >= min2 >= mg2 and gets t = mg2, so bits(mg1) + bits(mg2) - bits(t) is mg2 for the
+    // first and mg1 for the others (non-negative floats order and subtract as integers; ties give
+    // mg1 == mg2).  One half-rate min and a full-rate v_sub_u32 instead of v_cmp_eq into an SGPR pair
+    // (with its s_nop) and v_cndmask.
+    const uint32_t ms_ = __float_as_uint(mg1) + __float_as_uint(mg2);
+    auto magsel = [&](float x) {
+        float t;
+        asm("v_min_f32_e64 %0, |%1|, %2" : "=v"(t) : "v"(x), "v"(mg2));
+        return __uint_as_float(ms_ - __float_as_uint(t));
     };
 #else
     auto magsel = [&](float x) { return fabsf(x) == min1 ? mg2 : mg1; };

@@ -23,10 +23,14 @@ What is different from the reference and why:
     reach that call's graph, which a completed backward has already freed).  The final boundary of a
     call, self.llr[last + 1], is that call's own output state and stays attached to its graph, as the
     reference's self.llr[t + 1] does: resuming from it after a completed backward fails the same way
-    in both ("backward through the graph a second time").
+    in both ("backward through the graph a second time").  Exception: when that boundary is
+    self.llr[T] (the call ran up to the last iteration), no later call can resume from it, so the
+    fused kernel does not write it (65 536 codewords x E x Z = 19.8 GB at BG2 z=384) and it is
+    recomputed on demand, as a constant, if read.
   * gradients flow through the message state between the segments of one call (list-valued xa: one
     segment per iteration; split iteration lists), as through the reference's self.llr[t + 1].
 """
+import dataclasses
 from typing import Optional
 
 import torch
@@ -121,7 +125,7 @@ class BoostedNeuralLDPCDecoder(nn.Module):
                     raise RuntimeError(f"self.llr[{k}] cannot be recomputed: the state its run started from was "
                                        "modified in place after the call that recorded it")
                 w = lambda a: None if a is None else a[:off]  # noqa: E731
-                cfg = rec["cfg"]
+                cfg = dataclasses.replace(rec["cfg"], keep_state=True)
                 _, st = decode_autograd(self.conn_mat.graph, cfg, rec["x"], off, w_cn=w(rec["w_cn"]),
                                         w_ucn=w(rec["w_ucn"]),
                                         w_vn=None if rec["w_vn"] is None else rec["w_vn"][:cfg.vn_prefix + off],
@@ -345,8 +349,13 @@ class BoostedNeuralLDPCDecoder(nn.Module):
             w_vn = [weights[t][2] for t in run]
             has_vn = w_vn[0] is not None
             prefix = [] if listed else vn_hist
+            # a run that ends at the last iteration leaves a state no iteration resumes from (self.llr[T]):
+            # the fused kernel does not write it (19.8 GB per cfg3 launch); it stays readable, recomputed
+            # on demand like the run's inner boundaries
+            last = run[-1] == self.iter_node_counts - 1
             cfg = DecodeCfg(kind=kind, qbit=qbit, ucn=w_ucn[0] is not None, vn_cumulative=has_vn, llr_lo=lo,
-                            llr_hi=hi, first_iter=run[0], vn_prefix=len(prefix) if has_vn else 0)
+                            llr_hi=hi, first_iter=run[0], vn_prefix=len(prefix) if has_vn else 0,
+                            keep_state=not last)
             stack = lambda ws: torch.stack(ws) if ws[0] is not None else None  # noqa: E731
             w_vn_all = torch.stack(prefix + w_vn) if has_vn else None
             app_prev = None
@@ -359,9 +368,10 @@ class BoostedNeuralLDPCDecoder(nn.Module):
                                           c2v=state_in, app_prev=app_prev)
             for t, o in zip(run, outs):
                 self.outputs[t] = o
-            live[run[-1] + 1] = state
-            self.llr[run[-1] + 1] = state
-            if len(run) > 1:  # the boundaries inside the run: recomputed on demand (see the module docstring)
+            dropped = state.numel() == 0  # (the fused path skipped the final state: keep_state=False)
+            live[run[-1] + 1] = None if dropped else state
+            self.llr[run[-1] + 1] = None if dropped else state
+            if len(run) > 1 or dropped:  # boundaries inside the run (and a dropped final state): recomputed on demand
                 det = lambda a: None if a is None else a.detach()  # noqa: E731
                 # the input and previous posterior are copied (the caller may refill them in place: a
                 # 1/T-size copy beside the T outputs); the starting state is module-owned, its version
@@ -370,7 +380,7 @@ class BoostedNeuralLDPCDecoder(nn.Module):
                        "w_vn": det(w_vn_all), "state_in": det(state_in),
                        "state_ver": None if state_in is None else state_in._version,
                        "app_prev": None if app_prev is None else app_prev.clone()}
-                for off in range(1, len(run)):
+                for off in range(1, len(run) + (1 if dropped else 0)):
                     self.llr[run[0] + off] = BoostedNeuralLDPCDecoder._Pending(rec, off)
             if has_vn and not listed:
                 vn_hist = vn_hist + w_vn

@@ -35,7 +35,6 @@ class NeuralLDPCDecoder(nn.Module):
         self.biases_var = nn.ParameterList(
             [nn.Parameter(torch.zeros(E, dtype=torch.float32)) for _ in range(iter_node_counts)])
         self._cfg = DecodeCfg(kind=KIND_NEURAL, keep_state=False)  # forward() never resumes from a state
-        self._wb_cache = None  # (key, w [T, E], b [T, E]) for calls that record no autograd graph
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
                               error_msgs):
@@ -45,19 +44,11 @@ class NeuralLDPCDecoder(nn.Module):
                                       error_msgs)
 
     def _weights(self):
-        """The per-iteration weights and biases as [T, E] tensors.  When no autograd graph is recorded
-        (torch.no_grad, or no parameter requires grad) the stacked copies are kept and reused until a
-        parameter changes (storage or in-place version: optimizer steps, load_state_dict), so a serving
-        loop's decode is one kernel launch instead of three."""
-        ps = list(self.weights_var) + list(self.biases_var)
-        if torch.is_grad_enabled() and any(p.requires_grad for p in ps):
-            self._wb_cache = None
-            return torch.stack(list(self.weights_var)), torch.stack(list(self.biases_var))
-        key = tuple((p.data_ptr(), p._version, p.device) for p in ps)
-        if self._wb_cache is None or self._wb_cache[0] != key:
-            with torch.no_grad():
-                self._wb_cache = (key, torch.stack(list(self.weights_var)), torch.stack(list(self.biases_var)))
-        return self._wb_cache[1], self._wb_cache[2]
+        """The per-iteration weights and biases as [T, E] tensors, stacked on every call.  (A cache keyed
+        on the parameters' storage and in-place version missed updates made through `p.data`, which
+        do not bump the version -- the reference itself clamps parameters that way, Boosted…py:177 --
+        so a serving loop could have decoded with stale weights; the two stack launches cost ~10 us.)"""
+        return torch.stack(list(self.weights_var)), torch.stack(list(self.biases_var))
 
     def forward(self, xa):
         T = self.iter_node_counts

@@ -70,7 +70,7 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
     c = cfg.c_struct(c2v_in)
     L = _lib.lib()
     h = graph.handle(dev)
-    if cfg.path != "stream" and not c2v_in and T <= 64:  # a graph the library has no kernel for: compile one
+    if cfg.path != "stream" and not c2v_in and T <= 64 and jit.wanted(cfg):  # no built-in kernel: compile one
         jit.ensure(graph, dev, cfg.kind, 1 if save else 0)
     fast = ctypes.c_int32(0)
     _lib.check(L.nldpc_fast_path(h, ctypes.byref(c), B, T, int(bool(save)), ctypes.byref(fast)), "nldpc_fast_path")
@@ -118,7 +118,7 @@ def decode_count(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *
     h = graph.handle(dev)
     yb = None if y is None else (y != 0).to(torch.uint8).reshape(B, graph.N * graph.Z).contiguous()
     mode = 3 if (yb is not None or convention) else 2  # the count-only kernel variant
-    if cfg.path != "stream" and T <= 64 and not (cfg.ucn and cfg.first_iter > 0):
+    if cfg.path != "stream" and T <= 64 and not (cfg.ucn and cfg.first_iter > 0) and jit.wanted(cfg):
         jit.ensure(graph, dev, cfg.kind, mode)
     fast = ctypes.c_int32(0)
     _lib.check(L.nldpc_fast_path(h, ctypes.byref(c), B, T, mode, ctypes.byref(fast)), "nldpc_fast_path")
@@ -155,8 +155,7 @@ def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, 
     c = cfg.c_struct(c2v_in)
     L = _lib.lib()
     h = graph.handle(dev)
-    qms_identity = cfg.kind == KIND_QMS and cfg.qbit not in (6, 5, -5, 4, 3)
-    if (cfg.path != "stream" and not cfg.ucn and cfg.vn_prefix == 0 and T <= 64 and not qms_identity
+    if (cfg.path != "stream" and not cfg.ucn and cfg.vn_prefix == 0 and T <= 64 and jit.wanted(cfg)
             and grad_state is None and not want_state_grad and not c2v_in):  # the fused backward's conditions
         jit.ensure(graph, dev, cfg.kind, 4)
     nbytes = ctypes.c_size_t(0)

@@ -11,17 +11,23 @@ handle (nldpc_graph_attach_kernel).  Later decodes, in this process or another, 
 
 Modes: 0 decode, 1 decode + save for backward, 2 / 3 count-only, 4 backward (include/nldpc.h).
 Environment: NLDPC_JIT=0 disables compiling (graphs without a built-in kernel stream);
-NLDPC_JIT_CACHE=<dir> moves the cache (default: lib/jit next to libnldpc.so, else ~/.cache/nldpc-jit).
+NLDPC_JIT_CACHE=<dir> moves the cache (default: lib/jit next to libnldpc.so, else ~/.cache/nldpc-jit);
+NLDPC_JIT_LOG=<file> appends one line per compile (also logged on the "nldpc.jit" logger and kept in
+`compile_log`).  Any failure to build (no geometry, no hipcc, no generator sources, an unwritable cache,
+a compiler error) warns once and leaves that kernel to the streaming path.
 """
 from __future__ import annotations
 
 import ctypes
 import hashlib
 import importlib.util
+import logging
 import os
+import shutil
 import subprocess
 import tempfile
 import threading
+import time
 import warnings
 
 from . import _lib
@@ -37,6 +43,9 @@ _HEADERS = ("nldpc_fused.h", "nldpc_node.h", "nldpc_math.h", "nldpc_internal.h",
 _lock = threading.Lock()
 _gen = None
 _failed = set()  # (graph key, kind, mode) that could not be built: not retried in this process
+_log = logging.getLogger("nldpc.jit")
+# one dict per compile in this process: Z, kind, mode, geometry, seconds (profiles/ records them)
+compile_log: list = []
 
 
 def enabled() -> bool:
@@ -89,19 +98,42 @@ def code_object(basegraph, Z: int, kind: int, mode: int):
     src, geo = gen.jit_source(basegraph, int(Z), int(kind), int(mode))
     path = os.path.join(cache_dir(), f"fx_{_key(src)}.co")
     if not os.path.exists(path):
+        exe = HIPCC if os.path.isabs(HIPCC) else shutil.which(HIPCC)
+        if not exe or not os.path.exists(exe):
+            raise _lib.NldpcError(f"no hipcc at {HIPCC} to compile the run-time kernel (Z={Z})")
+        t0 = time.perf_counter()
         with tempfile.TemporaryDirectory() as tmp:
             s = os.path.join(tmp, "k.hip")
             with open(s, "w") as f:
                 f.write(src)
             out = os.path.join(tmp, "k.co")
-            r = subprocess.run([HIPCC, *FLAGS, s, "-o", out], capture_output=True, text=True)
+            r = subprocess.run([exe, *FLAGS, s, "-o", out], capture_output=True, text=True)
             if r.returncode != 0 or not os.path.exists(out):
                 raise _lib.NldpcError(f"hipcc failed on the run-time kernel (Z={Z}, kind {kind}, mode {mode}):\n"
                                       f"{r.stderr[-3000:]}")
             part = path + f".{os.getpid()}.tmp"
             os.replace(out, part)
             os.replace(part, path)  # atomic: a concurrent process sees the whole file or none
+        rec = {"Z": int(Z), "kind": int(kind), "mode": int(mode), "G": geo["G"], "P": geo["P"], "Q": geo["Q"],
+               "threads": geo["threads"], "padded": bool(geo["padded"]),
+               "seconds": round(time.perf_counter() - t0, 3)}
+        compile_log.append(rec)
+        line = (f"nldpc.jit: compiled Z={rec['Z']} kind={rec['kind']} mode={rec['mode']} (G={rec['G']} P={rec['P']} "
+                f"Q={rec['Q']} threads={rec['threads']}{' padded' if rec['padded'] else ''}) in {rec['seconds']:.2f} s")
+        _log.info(line)
+        if os.environ.get("NLDPC_JIT_LOG"):
+            with open(os.environ["NLDPC_JIT_LOG"], "a") as f:
+                f.write(line + "\n")
     return path, geo
+
+
+def wanted(cfg) -> bool:
+    """Whether the fused path could take a decode at all (so a run-time compile can pay off): not when
+    NLDPC_DISABLE_FUSED is set, and not for QMS with a quantiser the fused QMS kernels do not carry (an
+    inactive qbit decodes on the streaming kernels)."""
+    if os.environ.get("NLDPC_DISABLE_FUSED") is not None:
+        return False
+    return not (cfg.kind == _lib.NLDPC_QMS and cfg.qbit not in (6, 5, -5, 4, 3))
 
 
 def ensure(graph, device, kind: int, mode: int) -> bool:
@@ -125,9 +157,12 @@ def ensure(graph, device, kind: int, mode: int) -> bool:
             _failed.add(key)
             warnings.warn(f"nldpc: no fused kernel for Z={graph.Z} ({e}); decoding on the streaming kernels")
             return False
-        except _lib.NldpcError as e:
+        except (_lib.NldpcError, OSError, subprocess.SubprocessError) as e:
+            # no hipcc / no generator sources (an installed package without csrc/) / an unwritable cache /
+            # a compiler error: this kernel streams for the rest of the process
             _failed.add(key)
-            warnings.warn(f"nldpc: {e}; decoding on the streaming kernels")
+            warnings.warn(f"nldpc: no run-time kernel for Z={graph.Z} kind {kind} mode {mode} ({e}); "
+                          "decoding on the streaming kernels")
             return False
         with open(path, "rb") as f:
             data = f.read()

@@ -146,6 +146,30 @@ def test_boosted_train_step_grads(golden, name):
     assert n > 0
 
 
+def test_neural_no_grad_forward_sees_data_mutations():
+    """parameters changed through `p.data` (the reference clamps its weights that way,
+    Boosted…py:177) between two torch.no_grad() forwards are the ones the second decode uses -- no
+    stacked-weight cache can go stale."""
+    import neural_ldpc_decoder as nd
+    conn = nd.ConnectingMatrixTorch(nd.ConnectingMatrix(16, BG2), device=DEV)
+    gen = torch.Generator().manual_seed(3)
+    x = (2.0 * torch.randn(4, 52, 16, generator=gen) + 1.0).to(DEV)
+    model = nd.NeuralLDPCDecoder(5, 4, conn).to(DEV)
+    ref = nd.NeuralLDPCDecoder(5, 4, conn).to(DEV)
+    with torch.no_grad():
+        for t in range(5):
+            ref.weights_var[t].fill_(0.25)
+            ref.biases_var[t].fill_(-0.125)
+        a = model(x)[-1].clone()
+        for t in range(5):
+            model.weights_var[t].data.clamp_(0.0, 0.25)   # 0.5 -> 0.25, no _version bump
+            model.biases_var[t].data.sub_(0.125)
+        b = model(x)[-1].clone()
+        c = ref(x)[-1].clone()
+    assert not torch.equal(a, b)
+    assert torch.equal(b.view(torch.int32), c.view(torch.int32))
+
+
 def test_evaluate_ber_fer_literal(golden):
     from boosted_neural_ldpc_decoder import Functions
     d = golden("ber_values")

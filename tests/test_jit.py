@@ -54,3 +54,48 @@ def test_jit_compiles_a_code_object(tmp_path, monkeypatch):
     again, _ = jit.code_object(BG2, 52, 3, 0)  # a cache hit: same file, no recompile
     assert again == path
     shutil.rmtree(tmp_path, ignore_errors=True)
+
+
+def test_missing_hipcc_falls_back_to_streaming(monkeypatch):
+    """a host without the ROCm SDK (no hipcc) must not make decode() raise -- ensure() warns,
+    remembers the failure and returns False, so the decode streams.  code_object raises NldpcError
+    before touching the compiler; ensure() is driven here with a stand-in handle (no GPU on this host)."""
+    from nldpc import _lib, jit
+    from nldpc.graph import LiftedGraph
+    monkeypatch.setattr(jit, "HIPCC", "/nonexistent/hipcc")
+    monkeypatch.setenv("NLDPC_JIT_CACHE", "/tmp/nldpc-jit-test-nohipcc")
+    with pytest.raises(_lib.NldpcError, match="no hipcc"):
+        jit.code_object(BG2, 44, 3, 0)
+    g = LiftedGraph(BG2, 44)
+    monkeypatch.setattr(g, "handle", lambda dev: 1)
+    monkeypatch.setattr(jit, "kernel_mask", lambda h: 0)
+    jit._failed.clear()
+    with pytest.warns(UserWarning, match="streaming"):
+        assert jit.ensure(g, "cuda", 3, 0) is False
+    assert jit.ensure(g, "cuda", 3, 0) is False  # remembered: no second attempt, no second warning
+
+
+def test_unreadable_generator_sources_fall_back(monkeypatch, tmp_path):
+    """An installed package without csrc/ (OSError opening the generator or the headers) streams too."""
+    from nldpc import jit
+    from nldpc.graph import LiftedGraph
+    monkeypatch.setattr(jit, "CSRC", str(tmp_path / "missing"))
+    monkeypatch.setattr(jit, "_gen", None)
+    g = LiftedGraph(BG2, 36)
+    monkeypatch.setattr(g, "handle", lambda dev: 1)
+    monkeypatch.setattr(jit, "kernel_mask", lambda h: 0)
+    jit._failed.clear()
+    with pytest.warns(UserWarning, match="streaming"):
+        assert jit.ensure(g, "cuda", 3, 0) is False
+
+
+def test_wanted_skips_kernels_the_fused_path_never_takes(monkeypatch):
+    """decode() asks for a run-time compile only when the fused path could take the call."""
+    from nldpc import jit
+    from nldpc.decode import KIND_NEURAL, KIND_QMS, DecodeCfg
+    monkeypatch.delenv("NLDPC_DISABLE_FUSED", raising=False)
+    assert jit.wanted(DecodeCfg(kind=KIND_NEURAL))
+    assert jit.wanted(DecodeCfg(kind=KIND_QMS, qbit=5))
+    assert not jit.wanted(DecodeCfg(kind=KIND_QMS, qbit=7))  # identity quantiser: streaming kernels only
+    monkeypatch.setenv("NLDPC_DISABLE_FUSED", "1")
+    assert not jit.wanted(DecodeCfg(kind=KIND_NEURAL))

@@ -1,14 +1,23 @@
-# GPU-box A/B of experiment builds (tools/exp_build.sh): the cfg3 decode kernel time of each variant,
-# measured by bench.py with the variant's library.  VARIANTS="base cn4 ..." (lib_exp/<name>).
+# GPU-box A/B of experiment builds (tools/exp_build.sh): for each variant, the fused kernels checked bit for
+# bit against the streaming kernels of the same library (tools/ab_check.py), then the cfg3 decode kernel
+# time measured by bench.py with the variant's library.  VARIANTS="base cn4 ..." (lib_exp/<name>);
+# ROUNDS=2 runs the whole list twice (interleaved, to see box drift).
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
 cd $R
+for rnd in $(seq 1 ${ROUNDS:-1}); do
 for v in ${VARIANTS}; do
-    NLDPC_LIB_PATH=$R/neural-ldpc-decoder-torch_amd/lib_exp/$v/libnldpc.so timeout -k 10 240 python -u bench.py --steps ${STEPS:-6} --warmup 2 \
+    L=$R/neural-ldpc-decoder-torch_amd/lib_exp/$v/libnldpc.so
+    if [ -z "${NOCHECK}" ]; then
+        NLDPC_LIB_PATH=$L timeout -k 10 180 python -u tools/ab_check.py ${CHECK_KINDS} > $O/abchk_$v.log 2>&1 || { echo "$v check failed rc=$?"; tail -5 $O/abchk_$v.log; exit 1; }
+    fi
+    NLDPC_LIB_PATH=$L timeout -k 10 240 python -u bench.py --steps ${STEPS:-6} --warmup 2 \
         --no-cpu-baseline --no-sweep --no-count-only ${BENCH_ARGS} > $O/ab_$v.log 2>&1 || { echo "$v failed rc=$?"; tail -5 $O/ab_$v.log; exit 1; }
-    python3 - $v $O/ab_$v.log <<'PY'
-import json, sys
+    python3 - $v $O/ab_$v.log $O/abchk_$v.log <<'PY'
+import json, os, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-print(f"{sys.argv[1]:12s} {d['value']:>12.0f} cw/s  kernel {d['roofline']['avg_launch_ms']:.3f} ms  median step {d['ms_per_step_median']:.3f} ms")
+chk = open(sys.argv[3]).read().strip().splitlines()[-1] if os.path.exists(sys.argv[3]) else ""
+print(f"{sys.argv[1]:12s} {d['value']:>12.0f} cw/s  kernel {d['roofline']['avg_launch_ms']:.3f} ms  median step {d['ms_per_step_median']:.3f} ms  | {chk}")
 PY
+done
 done

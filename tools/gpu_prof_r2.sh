@@ -13,10 +13,14 @@ run() {  # name, timeout, rocprof args..., -- command
 B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-sweep --no-count-only"
 [ -n "$NO_PROBE" ] || run probe_fetch 120 --pmc FETCH_SIZE --kernel-trace -d $O/${TAG}_probe_fetch -o run --output-format csv -- python3 $R/tools/probe_pmc.py
 [ -n "$NO_PROBE" ] || run probe_write 120 --pmc WRITE_SIZE --kernel-trace -d $O/${TAG}_probe_write -o run --output-format csv -- python3 $R/tools/probe_pmc.py
-for W in ${WORKLOADS:-cfg3 cfg5}; do
-    run ${W}_trace 300 --kernel-trace --stats -d $O/${TAG}_${W}_trace -o run --output-format csv -- $B --workload $W
-    run ${W}_fetch 300 --pmc FETCH_SIZE --kernel-trace -d $O/${TAG}_${W}_fetch -o run --output-format csv -- $B --workload $W --no-profile
-    run ${W}_write 300 --pmc WRITE_SIZE --kernel-trace -d $O/${TAG}_${W}_write -o run --output-format csv -- $B --workload $W --no-profile
-    run ${W}_sq 300 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/${TAG}_${W}_sq -o run --output-format csv -- $B --workload $W --no-profile
+# WORKLOADS entries: cfg3 | cfg5 | cfg2 | cfg3ucn@KIND@CN,UCN,VN (a Boosted side line, e.g. cfg3ucn@QMS@1,1,2)
+for WS in ${WORKLOADS:-cfg3 cfg5}; do
+    IFS=@ read -r W K NW <<< "$WS"
+    A="--workload $W"; N=$W
+    if [ -n "$K" ]; then A="$A --kind $K --nw $NW"; N=${W}_${K}_NW${NW//,/}; fi
+    run ${N}_trace 300 --kernel-trace --stats -d $O/${TAG}_${N}_trace -o run --output-format csv -- $B $A
+    run ${N}_fetch 300 --pmc FETCH_SIZE --kernel-trace -d $O/${TAG}_${N}_fetch -o run --output-format csv -- $B $A --no-profile
+    run ${N}_write 300 --pmc WRITE_SIZE --kernel-trace -d $O/${TAG}_${N}_write -o run --output-format csv -- $B $A --no-profile
+    run ${N}_sq 300 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/${TAG}_${N}_sq -o run --output-format csv -- $B $A --no-profile
 done
 echo "all passes done"

@@ -46,6 +46,10 @@ out["calibration"] = {
 KERNELS = {"cfg3": [("fused", "fused_bg2_z384::kernel<3, 0>", 65536)],
            "cfg5": [("fused", "fused_bg2_z384::kernel<2, 1>", 2048), ("fusedb", "_bg2_z384::bwd_kernel<2>", 2048)],
            "cfg3ucn": [("fused", "fused_bg2_z384::kernel<1, 0>", 65536)]}
+# Boosted side lines, one entry per (kind, sharing codes): bench.py --workload cfg3ucn --kind K --nw a,b,c
+for _k, _kind in (("MS", 1), ("QMS", 2), ("SP", 0)):
+    for _nw in ("112", "100", "102", "110"):
+        KERNELS[f"cfg3ucn_{_k}_NW{_nw}"] = [("fused", f"fused_bg2_z384::kernel<{_kind}, 0>", 65536)]
 for w, ks in KERNELS.items():
     if not os.path.isdir(os.path.join(root, f"{tag}_{w}_sq")):
         continue
