@@ -136,6 +136,36 @@ CNBAL_ALPHA = float(os.environ.get("NLDPC_GEN_CNBAL_ALPHA", "0"))
 # heaviest waves are not left to finish alone at the phase's end (issue is arbitrated by priority, then age)
 PRIO = os.environ.get("NLDPC_GEN_PRIO", "0") == "1"
 
+# QMS variable nodes by total minus own message (1, default): every QMS VN input (the quantised channel
+# value or xin, and the quantised check messages) lies on the quantiser's 0.5 grid with magnitude <= 15.5,
+# so every partial sum of a column (<= 24 terms) is exact in fp32 and any summation order gives the
+# reference's sequential sum bit for bit: v2c_k = (x0 + C) - c_k with C = ((0 + c_0) + c_1) + ... (the
+# posterior's own sum), 2d + 1 adds per column copy instead of d(d-1)/2 + 2d.  (A zero result is +0 in
+# both forms; the check node's conditioning maps either zero to +1e-4 anyway.)
+QEXACT = os.environ.get("NLDPC_GEN_QEXACT", "1") == "1"
+
+# degree-1 bypass for the Boosted MS / QMS decode kernels too (1, default; Neural always has it): the
+# check-node thread holds each degree-1 edge's channel value (xin, advanced by the cumulative VN weights
+# in place), forms its v2c, its posterior and -- UCN -- its hard decision (kept in a register bit mask:
+# the same thread is the only reader of that bit in the next iteration), so those edges skip the LDS
+# round trip and the owner's divergent UCN bit updates
+D1B = os.environ.get("NLDPC_GEN_D1B", "1") == "1"
+
+# the tied-CN-weight backward kernels (MODE 5, default 1); experiment builds: NLDPC_GEN_TIED=0 leaves them out,
+# NLDPC_GEN_NOBWD=1 every backward kernel (decode-only A/B libraries compile in a fraction of the time)
+TIED_BWD = os.environ.get("NLDPC_GEN_TIED", "1") == "1"
+NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"
+
+# experiment knob: check-node writes (c2v back into the chunk image) by ds_write_addtid_b32 -- address = M0 +
+# offset + 4 * lane, no address VGPR, twice the LDS store rate of ds_write_b32 on gfx950
+# (tools/dev/addtid_probe.hip) -- on geometries whose waves hold 64 consecutive copies of one codeword
+CNTID = os.environ.get("NLDPC_GEN_CNTID", "0") == "1"
+
+# experiment knob: the owners' v2c writes into the chunk image by ds_write_addtid_b32 as well: no address VALU
+# at all (a copy whose shifted range wraps inside the wave writes twice, each half under its own EXEC mask
+# from the scalar unit), twice the LDS store rate; same geometries as CNTID
+OWNTID = os.environ.get("NLDPC_GEN_OWNTID", "0") == "1"
+
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
 
@@ -237,6 +267,11 @@ class Spec:
         # r3: off by default -- after the r3 kernel changes the per-copy form is faster for MS too (cfg3 MS
         # NW(1,1,2) + UCN kernel 111.6 -> 107.6 ms, same-box A/B, profiles/r3t_ab_ms_ucnw.txt)
         self.ucn_wave = self.ZT % 64 == 0 and Z % 32 == 0 and os.environ.get("NLDPC_GEN_UCNWAVE", "0") == "1"
+        # UCN hard decisions written by wave ballots (no LDS atomics, no clearing pass and barrier), the check
+        # side still gathering one bit per copy and edge: any geometry whose waves hold 64 consecutive copies
+        # of one codeword (the owner half of ucn_wave without its window-XOR check side)
+        self.ucn_bw = (not self.ucn_wave and self.ZT % 64 == 0 and Z % 32 == 0
+                       and os.environ.get("NLDPC_GEN_UCNBW", "0") == "1")
         self.lanes = G * self.ZT  # live threads per part
         # A part occupies whole waves.  The lanes past the live ones (padded parts) run the code of the
         # first live lanes (same copies) on an LDS region of their own and with global offsets out of
@@ -295,7 +330,7 @@ class Spec:
             4 if stage and all(o % 4 == 0 and n % 4 == 0 for o, n in blocks) else 0
         if stage and not self.stage_width:
             self.stage, self.stage_floats = 0, 0
-        self.nbuf = 2 if pipe else 1
+        self.nbuf = 2 if pipe and len(self.chunks) > 1 else 1  # (one chunk: the second buffer would stay unused)
         self.cn_rows = [balance(list(range(r0, r1)), lambda i: len(self.row_edges[i]), P)
                         for (r0, r1, _, _) in self.chunks]
         # forward check-node work units (row i, lane copy q) of each chunk, balanced over the parts by
@@ -352,7 +387,8 @@ def emit(S: Spec) -> str:
     w("#define SAVE (MODE == 1)")
     w("#define CNT (MODE >= 2)")
     w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
-    w("#define D1_BYPASS (KIND == NLDPC_NEURAL && !SAVE)")
+    d1b = D1B and not S.ucn_wave  # (the window-XOR UCN check side reads the degree-1 columns' LDS words)
+    w(f"#define D1_BYPASS ((KIND == NLDPC_NEURAL{' || KIND == NLDPC_MS || KIND == NLDPC_QMS' if d1b else ''}) && !SAVE)")
     w("// check-row LDS addresses from one 32-bit base (ROADDR); in the QMS / SP kernels it measured slower")
     w("#define ROA (KIND == NLDPC_NEURAL || KIND == NLDPC_MS)")
     w(f"#define UCNW ((KIND == NLDPC_MS{' || KIND == NLDPC_QMS' if UCNW_QMS else ''}) && {'true' if S.ucn_wave else 'false'})  "
@@ -440,6 +476,20 @@ def emit(S: Spec) -> str:
             for T_, arr, xin, g in grp:
                 ch = f"chan2<KIND>({xin}, a)" if T_ == "f2" else f"chan<KIND>({xin}, a)"
                 w(f"            const {T_} x0_{g} = {add(T_, zero(T_), ch) if ZADD else ch};")
+            def sub(T_, x, y):
+                return f"({x} - {y})" if T_ == "f2" else f"__fsub_rn({x}, {y})"
+            if QEXACT:  # QMS: exact sums on the quantiser's grid (see QEXACT)
+                w("            if constexpr (KIND == NLDPC_QMS) {")
+                for k in range(d):
+                    for T_, arr, xin, g in grp:
+                        pk = f"{arr}[{s + k}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k}]')
+                        w(f"                P_{g} = {pk};")
+                for T_, arr, xin, g in grp:
+                    w(f"                const {T_} tq_{g} = {add(T_, f'x0_{g}', f'P_{g}')};")
+                for k in range(d):
+                    for T_, arr, xin, g in grp:
+                        w(f"                {arr}[{s + k}] = {sub(T_, f'tq_{g}', f'{arr}[{s + k}]')};")
+                w("            } else {")
             # edges two at a time: the chains of k and k+1 (S_k from P_{k-1}, S_{k+1} from P_k) run
             # interleaved -- twice the independent adds per wave for the VN's dependent-add tail.
             # Chain k reads c_{k+1} first, before chain k+1 overwrites it with v2c_{k+1}.
@@ -477,6 +527,8 @@ def emit(S: Spec) -> str:
                         w(f"                asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]));")
                     for T_, arr, xin, g in grp:
                         w(f"                P_{g} = {add(T_, f'P_{g}', f'o_{g}')};")
+                w("            }")
+            if QEXACT:
                 w("            }")
         else:
             for k in range(d):
@@ -542,7 +594,9 @@ def emit(S: Spec) -> str:
                     if not final:
                         app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xs{i}[{n}], a))"
                         b_ = f"(it == 0 ? {app0} : y_) >= 0.f"
-                        if S.ucn_wave:
+                        if S.ucn_bw:
+                            w(f"            if (ucn_) app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {b_});")
+                        elif S.ucn_wave:
                             w(f"            if (ucn_) {{ if constexpr (UCNW) app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {b_}); "
                               f"else app_or(appw, {j * S.WZX}, u + {q * ZT}, {b_}); }}")
                         else:
@@ -553,13 +607,15 @@ def emit(S: Spec) -> str:
                 s += d
             if not final and S.d1_cols[p]:
                 # degree-1 columns: their posterior of iteration it-1 was formed in that iteration's read-back
-                # (rd_p), its hard decision kept in d1m
-                w("    if (ucn_) {")
+                # (rd_p), its hard decision kept in d1m (bypass: in the check-node thread's cdm instead)
+                w("    if (!D1_BYPASS && ucn_) {")
                 for n, j in enumerate(S.d1_cols[p]):
                     for q in range(Q):
                         app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xd[{n * Q + q}], a))"
                         bit = f"it == 0 ? {app0} >= 0.f : ((d1m >> {n * Q + q}) & 1u) != 0u"
-                        if S.ucn_wave:
+                        if S.ucn_bw:
+                            w(f"        app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {bit});")
+                        elif S.ucn_wave:
                             w(f"        if constexpr (UCNW) app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {bit}); "
                               f"else app_or(appw, {j * S.WZX}, u + {q * ZT}, {bit});")
                         else:
@@ -589,6 +645,25 @@ def emit(S: Spec) -> str:
         return (f"((lds_fp)(uintptr_t)((__builtin_amdgcn_inverse_ballot_w64(wrap_mask({Z - cq}, u0_)) ? lu1_ : lu0_) "
                 f"+ {4 * base}u))[0]")
 
+    def own_tid_write(e, q, e0, val):
+        """OWNTID: the owner's LDS write of (edge e, lane copy q) by ds_write_addtid_b32 at M0 = the wave's
+        LDS base (lane 0's copy) + the slot; a wrapped copy (lanes u >= T go Z slots back) writes twice,
+        lanes u < T and u >= T under their own EXEC (wrap_mask from the wave's first copy), EXEC restored."""
+        cq = (q * ZT - int(S.shift[e])) % Z
+        base = (e - e0) * Z + cq
+        w("    {")
+        if cq + ZT <= Z:
+            w(f"        asm volatile(\"s_mov_b32 m0, %0\\n\\ts_nop 0\\n\\tds_write_addtid_b32 %1\" :: \"s\"(slu_ + {4 * base}u), "
+              f"\"v\"({val}) : \"memory\", \"m0\");")
+        else:
+            w(f"        const uint64_t wm_ = wrap_mask({Z - cq}, su0_);  // lanes that wrap")
+            w("        uint64_t sv_;")
+            w("        asm volatile(\"s_mov_b64 %0, exec\\n\\ts_andn2_b64 exec, %0, %1\\n\\ts_mov_b32 m0, %2\\n\\ts_nop 0\\n\\t"
+              "ds_write_addtid_b32 %4\\n\\ts_and_b64 exec, %0, %1\\n\\ts_mov_b32 m0, %3\\n\\ts_nop 0\\n\\t"
+              "ds_write_addtid_b32 %4\\n\\ts_mov_b64 exec, %0\\n\\ts_nop 0\" : \"=&s\"(sv_) : \"s\"(wm_), "
+              f"\"s\"(slu_ + {4 * base}u), \"s\"(slu_ + {(4 * (base - Z)) & 0xFFFFFFFF}u), \"v\"({val}) : \"memory\", \"m0\");")
+        w("    }")
+
     def wrap_u0():  # before the asm barrier on u, so the compiler computes it once, not per phase
         if WRAPM:
             w("    const int u0_ = __builtin_amdgcn_readfirstlane(u) & ~63;  // the wave's first lane copy")
@@ -606,10 +681,16 @@ def emit(S: Spec) -> str:
             w(f"__device__ __forceinline__ void wr_p{p}_c{ci}({state_params(p, True)}, {x_params(p)}, float* lds, "
               f"int u, const FusedArgs& a, int it, rsrc_t sv, uint32_t vc) {{")
             wrap_u0()
+            if OWNTID and S.ZT % 64 == 0 and not S.padded and SAVECOPY:  # the wave's first copy and its LDS base
+                w("    const int su0_ = __builtin_amdgcn_readfirstlane(u);")
+                w("    const uint32_t slu_ = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u);")
             w("    asm volatile(\"\" : \"+v\"(u));  // LDS addresses are recomputed here, not hoisted out of the loop")
             wrap_prelude()
             for q in range(Q):
                 for k, e in mine:
+                    if OWNTID and S.ZT % 64 == 0 and not S.padded and SAVECOPY:
+                        own_tid_write(e, q, e0, ref(p, q, k))
+                        continue
                     w(f"    {own_lv(e, q, e0)} = {ref(p, q, k)};")
                     if not SAVECOPY:
                         w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(p, q, k)}, a.qp);")
@@ -703,11 +784,14 @@ def emit(S: Spec) -> str:
             w(f"__device__ __forceinline__ void cn_p{p}_c{ci}(float* lds, int u, const FusedArgs& a, int it, "
               f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last, "
               f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps, "
-              f"const uint32_t* appw) {{")
+              f"const uint32_t* appw, rsrc_t xr, rsrc_t apr, uint32_t& cdm) {{")
             wrap_u0()
             w("    asm volatile(\"\" : \"+v\"(u));")
             if ROADDR:
                 w("    const uint32_t lu_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u;")
+            tid = CNTID and S.ZT % 64 == 0 and not S.padded
+            if tid:  # the wave's copies are u0 + lane: its LDS base is lane 0's (M0 for ds_write_addtid_b32)
+                w("    const uint32_t slu_ = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u);")
             # row copies in order; weight offsets of each row in the preloaded W/Bv arrays
             rcs, woff, wo = list(S.cn_units[ci][p]), {}, 0
             for i in S.cn_order[(p, ci)]:
@@ -740,7 +824,7 @@ def emit(S: Spec) -> str:
                     w("    }")
                 for k, e in enumerate(es):
                     if e in d1set:
-                        w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = cd[{S.cd_index[p].index((e, q))}]; "
+                        w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = d1_v2c<KIND, {1 if ZADD else 0}>(cd[{S.cd_index[p].index((e, q))}], a); "
                           f"else m{n}[{k}] = rq{n}[{k * Z}];")
                     else:
                         w(f"    m{n}[{k}] = rq{n}[{k * Z}];")
@@ -778,10 +862,17 @@ def emit(S: Spec) -> str:
                     w("            else {")
                 w("            uint32_t par_ = 0;")
                 for k, e in enumerate(es):
-                    c, _ = rot(e, q)
+                    c, dvu = rot(e, q)
                     j = int(S.hb_cols[e])
                     vexpr = f"u + {c}" if c + ZT <= Z else f"u + {c} - (u >= {Z - c} ? {Z} : 0)"
-                    w(f"            {{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZX} + (v_ >> 5)] >> (v_ & 31); }}")
+                    rd_ = f"{{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZX} + (v_ >> 5)] >> (v_ & 31); }}"
+                    if e in d1set:  # bypass: the hard decision of this thread's own previous posterior
+                        ix = S.cd_index[p].index((e, q))
+                        app0 = f"(a.first_iter > 0 ? bload(apr, vo + {dvu}, {4 * (j * Z + c)}) : chan<KIND>(cd[{ix}], a))"
+                        w(f"            if constexpr (D1_BYPASS) par_ ^= it == 0 ? ({app0} >= 0.f ? 1u : 0u) : (cdm >> {ix}); "
+                          f"else {rd_}")
+                    else:
+                        w(f"            {rd_}")
                 w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
                 if S.ucn_wave:
                     w("            }")
@@ -797,14 +888,42 @@ def emit(S: Spec) -> str:
                     w(f"        if constexpr (KIND != NLDPC_NEURAL) cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
                 else:
                     w(f"        cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
+                if tid:  # every non-bypassed edge's c2v by one M0 and ds_write_addtid_b32 per edge
+                    wl = [(k, e) for k, e in enumerate(es) if e not in d1set]
+                    regs = ", ".join(f'"v"(m{n}[{k}])' for k, e in wl)
+                    ins = "\\n\\t".join(f"ds_write_addtid_b32 %{i + 1} offset:{4 * k * Z}" for i, (k, e) in enumerate(wl))
+                    cond = "if constexpr (!D1_BYPASS) " if any(e in d1set for e in es) else ""
+                    w(f"        {{ const uint32_t m0_ = slu_ + {4 * ((es[0] - e0c) * Z + q * ZT)}u;")
+                    if any(e in d1set for e in es):  # (no bypass: the degree-1 edges are written too)
+                        w("          if constexpr (!D1_BYPASS) {")
+                        for k, e in enumerate(es):
+                            if e in d1set:
+                                w(f"            rq{n}[{k * Z}] = m{n}[{k}];")
+                        w("          }")
+                    if wl:
+                        # (s_nop: one wait state between an M0 write and a DS *_ADDTID read of it on gfx9 -- the
+                        # hazard recognizer does not look inside inline asm)
+                        w(f"          asm volatile(\"s_mov_b32 m0, %0\\n\\ts_nop 0\\n\\t{ins}\" :: \"s\"(m0_), {regs} : \"memory\", \"m0\"); }}")
+                    else:
+                        w("        }")
                 for k, e in enumerate(es):
+                    if tid and e not in d1set:
+                        continue
                     if e in d1set:
                         j = int(S.hb_cols[e])
                         c, dv = rot(e, q, mask=True)
+                        ix = S.cd_index[p].index((e, q))
+                        pm = f"fadd(0.f, m{n}[{k}])" if ZADD else f"m{n}[{k}]"
                         w("        if constexpr (D1_BYPASS) {")
                         w(f"            const uint32_t dv_ = {dv};")
-                        w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, "
-                          f"fadd(cd[{S.cd_index[p].index((e, q))}], {'fadd(0.f, m' + str(n) + '[' + str(k) + '])' if ZADD else 'm' + str(n) + '[' + str(k) + ']'}), ps);")
+                        w("            float y_;")
+                        w(f"            if constexpr (KIND == NLDPC_NEURAL) y_ = fadd(cd[{ix}], {pm});")
+                        w("            else {  // Boosted: the unweighted channel value (cumulative VN weights: from memory)")
+                        w(f"                const float xo_ = a.w_vn ? bload(xr, vo + dv_, {4 * (j * Z + c)}) : cd[{ix}];")
+                        w(f"                y_ = posterior<KIND>(xo_, {pm}, a);")
+                        w(f"                if (a.ucn) cdm = (cdm & ~(1u << {ix})) | ((y_ >= 0.f ? 1u : 0u) << {ix});")
+                        w("            }")
+                        w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, y_, ps);")
                         w(f"            if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m{n}[{k}]);")
                         w(f"        }} else {{ rq{n}[{k * Z}] = m{n}[{k}]; }}")
                     elif "cnwrite" in SKIP:  # (timing experiment: keep the value live without the LDS write)
@@ -847,7 +966,9 @@ def emit(S: Spec) -> str:
                 w(f"    if ({g} < nlive) {{")
                 w("        if constexpr (KIND == NLDPC_QMS) {")
                 w(f"            int8_t* dst = (int8_t*)(svb + {(g * S.E + e0c) * Z});")
-                if NE % 16 == 0 and (g * CF * S.nbuf) % 4 == 0 and ((g * S.E + e0c) * Z) % 16 == 0:
+                # 16-byte stores only where every absolute address is 16-byte aligned: the saved buffer
+                # is 256-byte aligned, and iteration / block / codeword strides are multiples of E*Z bytes
+                if NE % 16 == 0 and (g * CF * S.nbuf) % 4 == 0 and ((g * S.E + e0c) * Z) % 16 == 0 and (S.E * Z) % 16 == 0:
                     w(f"            for (int i = t; i < {NE // 16}; i += {S.threads}) {{")
                     w(f"                const float4* s4 = (const float4*)({src} + 16 * i);")
                     w("                uint32_t o[4];")
@@ -863,7 +984,7 @@ def emit(S: Spec) -> str:
                     w(f"            for (int i = t; i < {NE}; i += {S.threads}) dst[i] = (int8_t)qms_code_p({src}[i], qp);")
                 w("        } else {")
                 w(f"            float* dst = (float*)(svb + {4 * (g * S.E + e0c) * Z});")
-                if NE % 4 == 0 and (g * CF * S.nbuf) % 4 == 0:
+                if NE % 4 == 0 and (g * CF * S.nbuf) % 4 == 0 and ((g * S.E + e0c) * Z) % 4 == 0 and (S.E * Z) % 4 == 0:
                     w(f"            for (int i = t; i < {NE // 4}; i += {S.threads}) "
                       f"reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>({src})[i];")
                 else:
@@ -967,7 +1088,8 @@ def emit(S: Spec) -> str:
         for idx, (e, q) in enumerate(S.cd_index[p]):
             c, dv = rot(e, q)
             # (0 + xa): the v2c of a degree-1 edge, canonical (never -0), as the check node sees it
-            w(f"        cd[{idx}] = fadd(0.f, bload(xr, vo + {dv}, {4 * (int(S.hb_cols[e]) * Z + c)}));")
+            w(f"        {{ const float x_ = bload(xr, vo + {dv}, {4 * (int(S.hb_cols[e]) * Z + c)}); "
+              f"cd[{idx}] = KIND == NLDPC_NEURAL ? fadd(0.f, x_) : x_; }}")
         w("    } else {")
         w(f"        for (int k = 0; k < {ncd}; ++k) cd[k] = 0.f;")
         w("    }")
@@ -983,6 +1105,11 @@ def emit(S: Spec) -> str:
             for n, j in enumerate(S.d1_cols[p]):
                 for q in range(Q):
                     w(f"{indent}  xd[{n * Q + q}] = chan_step<KIND>(xd[{n * Q + q}], a, wr_[{j}]);")
+            if S.cd_index[p]:  # (bypass: the degree-1 channel values the check-node thread holds)
+                w(f"{indent}  if constexpr (D1_BYPASS) {{")
+                for idx, (e, q) in enumerate(S.cd_index[p]):
+                    w(f"{indent}    cd[{idx}] = chan_step<KIND>(cd[{idx}], a, wr_[{int(S.hb_cols[e])}]);")
+                w(f"{indent}  }}")
             w(f"{indent}}}")
 
         def rs(ptr, size):  # descriptor over this block's part of a per-iteration buffer, or an empty one
@@ -1001,6 +1128,7 @@ def emit(S: Spec) -> str:
         # UCN: the hard-decision bit array of the codewords starts at zero (bits are OR-ed in); every later
         # iteration's array is cleared in the read-back phase of the iteration before
         w("    uint32_t d1m = 0;  // UCN: hard decisions of this thread's degree-1 posteriors")
+        w("    uint32_t cdm = 0;  // UCN, D1_BYPASS: hard decisions of the posteriors of this thread's cd entries")
         w(f"    const rsrc_t apr = make_rsrc(a.app_prev ? a.app_prev + blk * {NZ} : a.xa, a.app_prev ? nlive * {4 * NZ} : 0);")
         w("    if (KIND != NLDPC_NEURAL && a.ucn) {")
         w(f"        for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
@@ -1075,13 +1203,13 @@ def emit(S: Spec) -> str:
 
         def op_cn(ci):
             if "cn" not in SKIP:
-                w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw);")
+                w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw, xr, apr, cdm);")
 
         def op_r(ci):
             w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
               f"ps, d1m);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
-                w("        if (KIND != NLDPC_NEURAL && !UCNW && a.ucn) {")
+                w(f"        if (KIND != NLDPC_NEURAL && !UCNW && {'false' if S.ucn_bw else 'true'} && a.ucn) {{")
                 w(f"            for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
                 w("        }")
 
@@ -1121,7 +1249,7 @@ def emit(S: Spec) -> str:
             if K % 2 == 1:
                 w("        __syncthreads();")
             else:  # UCN: the bits cleared in R_{K-1} must be clear before any wave's next VN
-                w("        if (KIND != NLDPC_NEURAL && !UCNW && a.ucn) __syncthreads();")
+                w(f"        if (KIND != NLDPC_NEURAL && !UCNW && {'false' if S.ucn_bw else 'true'} && a.ucn) __syncthreads();")
         w("    }")
         w("    const float* pl = a.outs.p[a.T - 1];")
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
@@ -1137,6 +1265,7 @@ def emit(S: Spec) -> str:
         w("}")
     w("template <int KIND, int MODE>")
     w("__device__ __forceinline__ void kernel_body(const FusedArgs& a) {")
+    w("    if (a.sig != kFusedArgsSig) return;  // a launcher built against another FusedArgs layout")
     w(f"    __shared__ __attribute__((aligned(16))) float lds_all[{CF * S.G_lds * S.nbuf}];")
     w("    const int t = threadIdx.x;")
     w(f"    // every wave lies in one part ({S.lanes_pad} threads per part): the part is wave-uniform")
@@ -1237,6 +1366,8 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w(f"{indent}  bstore(cyr, vo, {X(j, q)}, du_ * wvn[{j}]); }}")
 
     def col_partial(j, indent):  # (lanes repeating a live one add nothing: Spec.lanes_pad)
+        # (a tied VN weight keeps these: one wave reduction per column either way; a per-lane running sum over
+        # the columns instead spilled 122 VGPRs)
         w(f"{indent}if (a.p_vn) {{ const float s_ = wave_sum(dup_ ? 0.f : ctb_); if (lane0) a.p_vn[pv + {j}] = s_; }}")
 
     # ---------------------------------------------------------------- LDS write / read-back
@@ -1255,7 +1386,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 for q in range(Q):
                     w(f"    lds[{own(e, q, e0)}] = gy_masked<KIND>(gr, mr, vo, vm, {X(j, q)});")
             w("}")
-            w("template <int KIND>")
+            w("template <int KIND, int TIED>")
             w(f"__device__ __forceinline__ void rdb_p{p}_c{ci}({state_params(p)}, const float* lds, "
               f"int u, const FusedBwdArgs& a, int it, uint32_t vo, rsrc_t xr, rsrc_t sxp, rsrc_t cyr, cfloat_p wvn, "
               f"int64_t pv, bool lane0, bool dup_) {{")
@@ -1280,7 +1411,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
 
     # ---------------------------------------------------------------- variable-node backward
     for p in range(S.P):
-        w("template <int KIND>")
+        w("template <int KIND, int TIED>")
         w(f"__device__ __forceinline__ void vnb_p{p}({state_params(p)}, const FusedBwdArgs& a, "
           f"int it, uint32_t vo, uint32_t vm, rsrc_t gr, rsrc_t mr, rsrc_t xr, rsrc_t sxp, rsrc_t cyr, cfloat_p wvn, "
           f"int64_t pv, bool lane0, bool dup_) {{")
@@ -1326,7 +1457,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     # check nodes), and each check copy reads its row's messages from LDS at h -- no global gathers in
     # the check-node phase.  Without staging they are read from global memory at h (coalesced).
     SBY = S.stage
-    w("template <int KIND, int DC>")
+    w("template <int KIND, int DC, int TIED>")
     w("__device__ __forceinline__ void cnb_row(float* rp, const char* sq, int u, const FusedBwdArgs& a, int it, "
       "int e0, int row, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
     w("    __builtin_amdgcn_sched_barrier(0);  // one row at a time (register pressure)")
@@ -1415,16 +1546,36 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 w(f"{indent}        }}")
             w(f"{indent}    }}")
             w(f"{indent}}}")
+    # tied CN weight (NLDPC_FLAG_CN_TIED): every edge's contribution joins the wave's running sum (one wave
+    # reduction per iteration, written by bwd_p into the part's designated edge); the row's entries get 0
+    def tied(indent, last):
+        # (one wave reduction per row copy into the wave's LDS sum: a per-lane running sum across the rows,
+        # no reduction inside the row loop, made the register allocator spill 5 520 VGPRs)
+        w(f"{indent}if constexpr (TIED) {{")
+        w(f"{indent}    float t_ = 0.f;")
+        w("#pragma unroll")
+        w(f"{indent}    for (int k = 0; k < DC; ++k) t_ += gwa[k];")
+        w(f"{indent}    const float s_ = wave_sum(dup_ ? 0.f : t_);")
+        w(f"{indent}    if (lane0) gacc[0] += s_;")
+        w(f"{indent}    if ({last} && lane0 && a.p_cn) {{")
+        w("#pragma unroll")
+        w(f"{indent}        for (int k = 0; k < DC; ++k) a.p_cn[pc + e0 + k] = 0.f;")
+        w(f"{indent}    }}")
+        w(f"{indent}}} else {{")
     if GWQ:
-        flush_q("        ")
+        tied("        ", f"q == {Q - 1}")
+        flush_q("            ")
+        w("        }")
     w("        __builtin_amdgcn_sched_barrier(0);  // one check copy at a time: the state owns the registers")
     w("    }")
     if not GWQ:
-        flush("    ")
+        tied("    ", "true")
+        flush("        ")
+        w("    }")
     w("}")
     for p in range(S.P):
         for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
-            w("template <int KIND>")
+            w("template <int KIND, int TIED>")
             w(f"__device__ __forceinline__ void cnb_p{p}_c{ci}(float* lds, const char* stg, int u, const FusedBwdArgs& a, "
               "int it, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
             w("    asm volatile(\"\" : \"+v\"(u));")
@@ -1433,7 +1584,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
             for i in rows:
                 es = S.row_edges[i]
                 off = (es[0] - e0c) * Z
-                w(f"    cnb_row<KIND, {len(es)}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, svr, vcw, pc, "
+                w(f"    cnb_row<KIND, {len(es)}, TIED>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, svr, vcw, pc, "
                   "lane0, dup_, gacc);")
             w("}")
             # the chunk's saved block -> this codeword's staging region (all threads of the workgroup)
@@ -1461,7 +1612,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     # ---------------------------------------------------------------- per-part driver
     for p in range(S.P):
         sp = max(len(S.slots[p]), 1)
-        w("template <int KIND>")
+        w("template <int KIND, int TIED>")
         w(f"__device__ __forceinline__ void bwd_p{p}(const FusedBwdArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"uint32_t vo, uint32_t vm, uint32_t vcw, int slot, bool lane0, bool dup_, const char* stg, char* stg_all, "
           f"float* gacc) {{")
@@ -1507,6 +1658,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 w(f"        if (a.stamps && blockIdx.x < 256 && (threadIdx.x & 63) == 0) "
                   f"a.stamps[((blockIdx.x * {S.threads // 64} + (threadIdx.x >> 6)) * a.T + it) * 16 + {ph}] = "
                   f"__builtin_amdgcn_s_memtime();")
+        w("        if (TIED && lane0) gacc[0] = 0.f;  // (tied CN: the wave's sum lives in its LDS slot)")
         bstamp(0)
         for ci in range(len(S.chunks)):
             if SBY:  # the chunk's saved messages start moving into LDS now and land by the barrier
@@ -1516,32 +1668,41 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
             if SBY:
                 w("        asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // (LDS-DMA: not in hipcc's count)")
             w("        __syncthreads();")
-            w(f"        cnb_p{p}_c{ci}<KIND>(lds, stg, u, a, it, svr, vcw, pc, lane0, dup_, gacc);")
+            w(f"        cnb_p{p}_c{ci}<KIND, TIED>(lds, stg, u, a, it, svr, vcw, pc, lane0, dup_, gacc);")
             bstamp(2 + 3 * ci)
             w("        __syncthreads();")
-            w(f"        rdb_p{p}_c{ci}<KIND>({state_args()}, lds, u, a, it, vo, xr, sxp, cyr, wvn, pv, lane0, dup_);")
+            w(f"        rdb_p{p}_c{ci}<KIND, TIED>({state_args()}, lds, u, a, it, vo, xr, sxp, cyr, wvn, pv, lane0, dup_);")
             bstamp(3 + 3 * ci)
             w("        __syncthreads();")
         w("        const float* gq_ = it >= 1 ? a.gy.p[it - 1] : nullptr;  // dL/dy_{k-1}")
         w("        const uint8_t* mq_ = (a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t gr1 = {rs('gq_', 4, NZ)};")
         w(f"        const rsrc_t mr1 = {rs('mq_', 1, NZ)};")
-        w(f"        vnb_p{p}<KIND>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0, dup_);")
+        w(f"        vnb_p{p}<KIND, TIED>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0, dup_);")
+        # tied weights: the wave's sums into the part's designated entries (written 0 earlier this iteration,
+        # by this wave's lane 0: program order makes these the final values)
+        rows_p = [sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i])) for ci in range(len(S.chunks))]
+        first = next((r[0] for r in rows_p if r), None)
+        if first is not None:
+            w(f"        if (TIED && a.p_cn && lane0) a.p_cn[pc + {S.row_edges[first][0]}] = gacc[0];")
+
         bstamp(1 + 3 * len(S.chunks))
         w("    }")
         w("}")
 
-    w("template <int KIND>")
-    w("__device__ __forceinline__ void bwd_body(const FusedBwdArgs& a) {")
+    w("template <int KIND, int TIED>")
+    w("__device__ __forceinline__ void bwd_body(const FusedBwdArgs& a, float* lds_sh) {")
+    w("    if (a.sig != kFusedBwdArgsSig) return;  // a launcher built against another FusedBwdArgs layout")
     STF = S.stage_floats
     if SBY:
         w(f"    static_assert(saved_msg_bytes<KIND>() == {SBY}, \"kernel built for another saved-message width\");")
-    GA = 2 * S.max_dc * (S.threads // 64) if GWQ and Q > 1 else 1
+    GST = 2 * S.max_dc if GWQ and Q > 1 else 1  # per-wave sums (lane 0): a row's copies, or the tied CN sum
+    GA = GST * (S.threads // 64)
     assert 4 * (STF * S.G_lds + CF * S.G_lds + GA) <= 160 * 1024, S.tag
-    w(f"    __shared__ __attribute__((aligned(16))) float lds_sh[{STF * S.G_lds + CF * S.G_lds + GA}];  // staging | images | sums")
+    w(f"    // lds_sh: [{STF * S.G_lds + CF * S.G_lds + GA}] floats, staging | images | sums (declared once in bwd_entry)")
     w(f"    char* stg_all = (char*)lds_sh;  // [G_lds][{4 * STF}] bytes: the chunk's saved messages (S.stage)")
     w(f"    float* lds_all = lds_sh + {STF * S.G_lds};")
-    w(f"    float* gacc = lds_sh + {STF * S.G_lds + CF * S.G_lds} + {2 * S.max_dc if GA > 1 else 0} * (threadIdx.x >> 6);  "
+    w(f"    float* gacc = lds_sh + {STF * S.G_lds + CF * S.G_lds} + {GST} * (threadIdx.x >> 6);  "
       "// this wave's weight-gradient sums over a row's copies (lane 0)")
     w("    const int t = threadIdx.x;")
     w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes_pad});")
@@ -1562,12 +1723,21 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     if SBY and S.padded:  # the repeating lanes' staging region is never filled: zeros, not stale LDS
         w(f"    for (int i = t; i < {STF}; i += {S.threads}) ((float*)(stg_all + {G * 4 * STF}))[i] = 0.f;")
     for p in range(S.P):
-        w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0, dup_, "
+        w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND, TIED>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0, dup_, "
           "stg, stg_all, gacc);")
     w("}")
-    w("template <int KIND>")
+    # a tied CN weight (cfg5's NW(3,0,3): one CN weight per iteration): a separate kernel (TIED = 1) reduces
+    # each row copy's contributions once (one wave reduction per row copy into the wave's LDS sum) instead of
+    # once per edge; the launcher takes it when the CN gradient is tied (nldpc_backward.hip).  (Both bodies behind a run-time branch in one
+    # kernel: 8 994 spilled VGPRs.)
+    w("template <int KIND, int TIED>")
+    w("__device__ __forceinline__ void bwd_entry(const FusedBwdArgs& a) {")
+    w(f"    __shared__ __attribute__((aligned(16))) float lds_sh[{STF * S.G_lds + CF * S.G_lds + GA}];")
+    w("    bwd_body<KIND, TIED>(a, lds_sh);")
+    w("}")
+    w("template <int KIND, int TIED>")
     w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void bwd_kernel(FusedBwdArgs a) {{")
-    w("    bwd_body<KIND>(a);")
+    w("    bwd_entry<KIND, TIED>(a);")
     w("}")
     w("}  // namespace")
     return "\n".join(L)
@@ -1600,7 +1770,7 @@ def jit_source(hb, Z, kind, mode):
                  f"nldpc::fused_jit::kernel_body<{kind}, {mode}>(a); }}")
     else:
         L.append(f'extern "C" __global__ {lb} void nldpc_fxb(nldpc::FusedBwdArgs a) {{ '
-                 f"nldpc::{BWD_NS[kind]}_jit::bwd_body<{kind}>(a); }}")
+                 f"nldpc::{BWD_NS[kind]}_jit::bwd_entry<{kind}, 0>(a); }}")
     return "\n".join(L) + "\n", {"G": G, "threads": S.threads, "waves_per_part": S.lanes_pad // 64,
                                  "P": P, "Q": Q, "padded": S.padded}
 
@@ -1661,17 +1831,24 @@ def main():
         # backward kernels: the fp32-message kinds and QMS (int8 codes) stage their saved messages in LDS
         # beside chunk images sized for them, so they are two generated namespaces
         src = list(head)
-        if on:
+        if on and not NOBWD:
             done = set()
             for k in kinds:
                 if BWD_NS[k] not in done:
                     done.add(BWD_NS[k])
                     src.append(emit_bwd(Spec(S.tag, S.hb, S.Z, S.G, S.P, S.Q, stage=BWD_STAGE[k]), BWD_NS[k]))
         src.append(f"void* fused_{S.tag}_bwd(int kind) {{")
-        if on:
+        if on and not NOBWD:
             for k in kinds:
                 nsk = BWD_NS[k]
-                src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&{nsk}_{S.tag}::bwd_kernel<{k}>);")
+                src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&{nsk}_{S.tag}::bwd_kernel<{k}, 0>);")
+        src.append("    return nullptr;")
+        src.append("}")
+        src.append(f"void* fused_{S.tag}_bwd_tied(int kind) {{  // a tied CN weight (NLDPC_FLAG_CN_TIED)")
+        if on and TIED_BWD and not NOBWD:
+            for k in kinds:
+                if k != 3:
+                    src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&{BWD_NS[k]}_{S.tag}::bwd_kernel<{k}, 1>);")
         src.append("    return nullptr;")
         src.append("}")
         src.append("}  // namespace nldpc")
@@ -1681,6 +1858,7 @@ def main():
         for v in MODES:
             src.append(f"void* fused_{S.tag}_kernel_s{v}(int kind);")
         src.append(f"void* fused_{S.tag}_bwd(int kind);")
+        src.append(f"void* fused_{S.tag}_bwd_tied(int kind);")
         src.append(f"static const int32_t basegraph_{S.tag}[{S.M * S.N}] = "
                    f"{{{', '.join(str(int(x)) for x in S.hb.reshape(-1))}}};")
     src.append("const FusedSpec* fused_specs(int* n) {")
@@ -1688,8 +1866,9 @@ def main():
     for S, _, _ in specs:
         ks = ", ".join("{" + ", ".join(f"fused_{S.tag}_kernel_s{v}({k})" for k in range(4)) + "}" for v in MODES)
         kb = ", ".join(f"fused_{S.tag}_bwd({k})" for k in range(4))
+        kt = ", ".join(f"fused_{S.tag}_bwd_tied({k})" for k in range(4))
         src.append(f"        {{\"{S.tag}\", {S.M}, {S.N}, {S.Z}, {S.E}, {S.G}, {S.threads}, basegraph_{S.tag}, "
-                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}}},")
+                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}, {{{kt}}}}},")
     src.append("    };")
     src.append(f"    *n = {len(specs)};")
     src.append("    return tab;")

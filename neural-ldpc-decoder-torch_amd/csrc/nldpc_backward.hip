@@ -413,13 +413,19 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
                           const float* w_cn, const float* bias, const float* w_vn, const float* const* grad_outs,
                           const void* saved, float* g_w_cn, float* g_bias, float* g_w_vn, void* work,
                           hipStream_t s) {
-    const FusedLaunch f = fused_launch(g, 4, cfg->kind);
+    // a tied CN weight (NLDPC_FLAG_CN_TIED) whose gradient is wanted: the kernel that reduces each row copy's
+    // contributions once (MODE 5); its partials put each iteration's totals into a few entries per row.  (A tied
+    // VN weight needs no other kernel: its partials are one wave reduction per column either way.)
+    const bool tied = cfg->kind != NLDPC_NEURAL && g_w_cn && w_cn && (cfg->flags & NLDPC_FLAG_CN_TIED);
+    const FusedLaunch ft = tied ? fused_launch(g, 5, cfg->kind) : FusedLaunch{};
+    const FusedLaunch f = ft ? ft : fused_launch(g, 4, cfg->kind);
     const FusedWork W = fused_work_layout(g, cfg, B, T);
     const SavedLayout SL = saved_layout(g, cfg, B, T);
     const DevGraph& G = g->dev;
     const char* sb = static_cast<const char*>(saved);
     char* wb = static_cast<char*>(work);
     FusedBwdArgs a{};
+    a.sig = kFusedBwdArgsSig;
     a.B = B;
     a.T = T;
     a.qbit = cfg->qbit;
@@ -442,6 +448,8 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
     a.p_vn = a.w_vn ? reinterpret_cast<float*>(wb + W.pvn_off) : nullptr;
     a.carry = a.w_vn ? reinterpret_cast<float*>(wb + W.carry_off) : nullptr;
     a.nslots = W.nslots;
+    a.cn_tied = ft ? 1 : 0;
+    a.vn_tied = 0;
     for (int k = 0; k < kFusedMaxT; ++k) a.gy.p[k] = k < T ? const_cast<float*>(grad_outs[k]) : nullptr;
     // diagnostic stamp build (lib_stamps/): NLDPC_STAMPS_BWD=<file> collects the phase stamps of each call
     static const char* stamp_file = std::getenv("NLDPC_STAMPS_BWD");

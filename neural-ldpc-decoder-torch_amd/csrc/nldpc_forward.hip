@@ -295,6 +295,7 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     const FusedLaunch f = fused_launch(g, mode, cfg->kind);
     if (!f) return fail(NLDPC_EUNSUPPORTED, "no register-resident kernel for this graph / mode / kind");
     FusedArgs fa{};
+    fa.sig = kFusedArgsSig;
     fa.B = B;
     fa.T = T;
     fa.qbit = cfg->qbit;

@@ -14,7 +14,15 @@ struct OutPtrs {
     float* p[kFusedMaxT];
 };
 
+// Launcher / kernel agreement on the argument structs: the host writes kFused*Sig into `sig` (the first
+// field, so any layout reads it), and a generated kernel whose compiled layout differs returns at once
+// instead of reading every later field at the wrong offset (r3: an experiment library whose kernels were
+// built against a newer FusedArgs than its launcher ran a loop bounded by a pointer's low word).  Bump
+// kFusedArgsVersion with every layout change that keeps the size.
+constexpr uint32_t kFusedArgsVersion = 5;
+
 struct FusedArgs {
+    uint32_t sig;        // kFusedArgsSig
     int64_t B;
     int32_t T;
     int32_t qbit;
@@ -43,6 +51,8 @@ struct FusedArgs {
     unsigned long long* cnt;  // [T][2] (+=) bit errors, frame errors
     uint64_t* stamps;    // diagnostic stamp build only (make STAMPS=1): [256][waves][T][16] s_memtime
 };
+
+constexpr uint32_t kFusedArgsSig = 0x4e4c0000u ^ ((uint32_t)sizeof(FusedArgs) << 4) ^ kFusedArgsVersion;
 
 // Global memory of the fused kernels goes through buffer descriptors built from wave-uniform values:
 // one 32-bit VGPR byte offset per lane serves every access (the per-column constant rides in the
@@ -129,6 +139,16 @@ __device__ __forceinline__ float posterior_m(float xav, float P, const FusedArgs
     const float yp = fadd(xo, P);
     m = yp >= a.lo && yp <= a.hi;
     return clampf(yp, a.lo, a.hi);
+}
+
+// v2c of a degree-1 edge from the channel value its check-node thread holds (degree-1 bypass): Neural
+// holds 0 + xa already; Boosted forms (0 + chan(xin)) + 0 as the owner's VN sum would (ZADD: the
+// reference's sums start from 0; a lone message adds nothing else)
+template <int KIND, int ZADD>
+__device__ __forceinline__ float d1_v2c(float cd, const FusedArgs& a) {
+    if constexpr (KIND == NLDPC_NEURAL) return cd;
+    const float x = chan<KIND>(cd, a);
+    return ZADD ? fadd(fadd(0.f, x), 0.f) : x;
 }
 
 template <int KIND>
@@ -545,6 +565,7 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
 // v2c / clamp masks / xin and the incoming output gradients.  Weight gradients go to per-wave
 // partial sums [T][nslots][E|N] reduced afterwards (nldpc_backward.hip).  vn_prefix must be 0.
 struct FusedBwdArgs {
+    uint32_t sig;          // kFusedBwdArgsSig (see kFusedArgsSig)
     int64_t B;
     int32_t T, qbit;
     float lo, hi;
@@ -563,9 +584,12 @@ struct FusedBwdArgs {
     float* p_vn;           // [T][nslots][N] or nullptr
     float* carry;          // [B][N][Z] VN-chain carry (workspace; written before it is read)
     int64_t nslots;
+    int32_t cn_tied, vn_tied;  // the MODE-5 (tied CN weight) kernel runs; vn_tied: reserved (0)
     OutPtrs gy;            // T output gradients [B][N][Z] (nullptr = zero)
     uint64_t* stamps;      // diagnostic stamp build only (make STAMPS=1): [256][waves][T][16] s_memtime
 };
+
+constexpr uint32_t kFusedBwdArgsSig = 0x4e420000u ^ ((uint32_t)sizeof(FusedBwdArgs) << 4) ^ kFusedArgsVersion;
 
 // LDS-DMA operands (__builtin_amdgcn_global_load_lds: global source per lane, wave-uniform LDS base)
 typedef __attribute__((address_space(1))) void* gptr_t;
@@ -809,11 +833,13 @@ struct FusedSpec {
     void* kernels[4][4];       // [MODE: decode / save / count / count against y][nldpc_kind]
     void* bwd[4];              // backward kernels [nldpc_kind]
     int32_t waves_per_part;    // partial-sum slots per workgroup
+    void* bwd_tied[4];         // backward kernels for tied CN / VN weights (MODE 5 in fused_launch), or nullptr
 };
 
 const FusedSpec* fused_specs(int* n);
 
-// How to launch the register-resident kernel of (graph, MODE, kind) (MODE 4: the backward): one compiled
+// How to launch the register-resident kernel of (graph, MODE, kind) (MODE 4: the backward; MODE 5: the
+// backward for tied weights, library kernels only -- a run-time compiled graph uses MODE 4): one compiled
 // into the library (fused_specs table, hipLaunchKernel) or one compiled at run time for this graph and
 // attached (nldpc_graph_attach_kernel, hipModuleLaunchKernel); empty when neither exists.
 struct FusedLaunch {

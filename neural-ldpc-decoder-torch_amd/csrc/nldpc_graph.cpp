@@ -249,15 +249,15 @@ extern "C" int nldpc_graph_create(int32_t M, int32_t N, int32_t Z, const int32_t
 namespace nldpc {
 FusedLaunch fused_launch(const nldpc_graph* g, int mode, int kind) {
     FusedLaunch L;
-    if (!g || mode < 0 || mode > 4 || kind < 0 || kind > 3) return L;
+    if (!g || mode < 0 || mode > 5 || kind < 0 || kind > 3) return L;
     if (g->fused >= 0) {
         int n = 0;
         const FusedSpec& f = fused_specs(&n)[g->fused];
-        L.host = mode == 4 ? f.bwd[kind] : f.kernels[mode][kind];
+        L.host = mode == 5 ? f.bwd_tied[kind] : mode == 4 ? f.bwd[kind] : f.kernels[mode][kind];
         L.G = f.G;
         L.threads = f.threads;
         L.waves_per_part = f.waves_per_part;
-    } else if (g->jit_fn[mode][kind]) {
+    } else if (mode < 5 && g->jit_fn[mode][kind]) {
         L.fn = g->jit_fn[mode][kind];
         L.G = g->jit_G;
         L.threads = g->jit_threads;

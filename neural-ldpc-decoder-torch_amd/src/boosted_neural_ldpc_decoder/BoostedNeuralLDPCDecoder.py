@@ -271,6 +271,11 @@ class BoostedNeuralLDPCDecoder(nn.Module):
             w_ucn = self._per_edge(self.fetch_param(ParamType.Weight, NodeType.UCN, it), cn, "UCN")
         return w_cn, w_ucn, w_vn
 
+    def _tied(self, node_type):
+        """Whether every per-edge weight row repeats one parameter: sharing code 3, one weight per
+        iteration (Boosted…py:114-124)."""
+        return self.node_weight_sharing_config.get(node_type) == 3
+
     @torch.no_grad()
     def count_errors(self, xa, y=None, convention=0):
         """Count-only decode (extension): int64 [T, 2] device tensor of (bit errors, frame
@@ -355,7 +360,7 @@ class BoostedNeuralLDPCDecoder(nn.Module):
             last = run[-1] == self.iter_node_counts - 1
             cfg = DecodeCfg(kind=kind, qbit=qbit, ucn=w_ucn[0] is not None, vn_cumulative=has_vn, llr_lo=lo,
                             llr_hi=hi, first_iter=run[0], vn_prefix=len(prefix) if has_vn else 0,
-                            keep_state=not last)
+                            keep_state=not last, cn_tied=self._tied(NodeType.CN))
             stack = lambda ws: torch.stack(ws) if ws[0] is not None else None  # noqa: E731
             w_vn_all = torch.stack(prefix + w_vn) if has_vn else None
             app_prev = None
@@ -364,6 +369,11 @@ class BoostedNeuralLDPCDecoder(nn.Module):
             # the state this run starts from: this call's own (differentiable) or a stored one (:343, :377)
             state_in = live[run[0]] if run[0] in live else self._state(run[0])
             wc, wu = stack(w_cn), stack(w_ucn)
+            # the entries this run rewrites let go of the previous call's outputs first (the list is refilled
+            # below, as the reference's :523 overwrites it): otherwise two T x [B, N*Z] buffers are alive at
+            # once (cfg3: 2 x 105 GB); a caller holding those tensors keeps them regardless
+            for t in run:
+                self.outputs[t] = None
             outs, state = decode_autograd(self.conn_mat.graph, cfg, x_in, len(run), w_cn=wc, w_ucn=wu, w_vn=w_vn_all,
                                           c2v=state_in, app_prev=app_prev)
             for t, o in zip(run, outs):

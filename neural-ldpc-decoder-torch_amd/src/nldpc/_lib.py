@@ -20,8 +20,8 @@ LIB_PATH = os.environ.get("NLDPC_LIB_PATH") or os.path.normpath(os.path.join(_HE
 
 NLDPC_OK, NLDPC_EINVAL, NLDPC_EHIP, NLDPC_EUNSUPPORTED = 0, 1, 2, 3
 NLDPC_SP, NLDPC_MS, NLDPC_QMS, NLDPC_NEURAL = 0, 1, 2, 3
-ABI_VERSION = 3
-FLAG_STREAM, FLAG_FUSED, FLAG_NO_STATE = 1, 2, 4
+ABI_VERSION = 4
+FLAG_STREAM, FLAG_FUSED, FLAG_NO_STATE, FLAG_CN_TIED = 1, 2, 4, 8
 
 # every symbol include/nldpc.h declares
 EXPORTED = (

@@ -30,9 +30,14 @@ class DecodeCfg:
     vn_prefix: int = 0
     path: str = "auto"        # "auto" | "stream" | "fused" (register-resident kernel)
     keep_state: bool = True   # False: the final c2v state is not needed (lets the fused path skip it)
+    # every row of w_cn repeats one weight (sharing code 3): the backward may put each iteration's gradient
+    # total into a few entries of the row (only row sums are meaningful, which is what the expand() that
+    # built the row passes on) -- NLDPC_FLAG_CN_TIED
+    cn_tied: bool = False
 
     def flags(self) -> int:
         f = {"auto": 0, "stream": _lib.FLAG_STREAM, "fused": _lib.FLAG_FUSED}[self.path]
+        f |= _lib.FLAG_CN_TIED if self.cn_tied else 0
         return f | (0 if self.keep_state else _lib.FLAG_NO_STATE)
 
     def c_struct(self, c2v_in: bool) -> _lib.NldpcCfg:

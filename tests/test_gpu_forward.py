@@ -472,25 +472,36 @@ def test_runtime_kernel_lifting_sizes_match_oracle(Z, kind):
     assert torch.equal(counts, ber_counts(list(outs)))
 
 
-def test_runtime_kernel_training_step_matches_streaming():
-    """The run-time compiled saving forward (mode 1) and backward (mode 4) at a lifting size with padded
-    parts (BG2 z=104, QMS q=5, per-edge CN and per-column VN weights): the same outputs and weight
-    gradients as the streaming kernels."""
+@pytest.mark.parametrize("kind,Z,B", [(2, 104, 4), (3, 52, 5), (1, 52, 5), (2, 15, 3), (3, 15, 3)])
+def test_runtime_kernel_training_step_matches_streaming(kind, Z, B):
+    """The run-time compiled saving forward (mode 1) and backward (mode 4) against the streaming kernels:
+    the same outputs and weight gradients.  Cases: BG2 z=104 QMS (padded parts); z=52 with an
+    odd batch (G=2 codewords per workgroup, a partial last workgroup whose missing codeword's lanes read
+    never-staged LDS) for Neural (fp32 LDS-staged backward, bias gradients) and MS; z=15 (odd Z: the
+    4-byte staging and scalar save paths) for QMS and Neural."""
     from nldpc.decode import DecodeCfg, decode, decode_backward
-    T, B, Z = 6, 4, 104
-    g = _graph(BG2, Z)
-    gen = torch.Generator().manual_seed(104)
     from oracle.ldpc_oracle import quantize
-    x = quantize((2 * (-1 + 0.85 * torch.randn(B, 52, Z, generator=gen)) / 0.7225).float(), 5).to(DEV)
+    T = 6
+    g = _graph(BG2, Z)
+    gen = torch.Generator().manual_seed(Z * 10 + kind)
+    x = (2 * (-1 + 0.85 * torch.randn(B, 52, Z, generator=gen)) / 0.7225).float()
+    if kind == 2:
+        x = quantize(x, 5)
+    x = x.to(DEV)
     wc = (0.5 + torch.rand(T, g.E, generator=gen)).to(DEV)
-    wv = (0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV)
     gy = [torch.randn(B, 52 * Z, generator=gen).to(DEV) for _ in range(T)]
+    if kind == 3:
+        kw = dict(w_cn=wc, bias=(0.2 * torch.randn(T, g.E, generator=gen)).to(DEV))
+        gi = (0, 2)
+    else:
+        kw = dict(w_cn=wc, w_vn=(0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV))
+        gi = (0, 3)
     res = {}
     for path in ("stream", "fused"):
-        cfg = DecodeCfg(2, qbit=5, vn_cumulative=True, path=path)
-        outs, _, saved = decode(g, cfg, x, T, w_cn=wc, w_vn=wv, save=True)
-        grads = decode_backward(g, cfg, x, T, gy, list(outs), saved, w_cn=wc, w_vn=wv)
-        res[path] = (outs, grads[0], grads[3])
+        cfg = DecodeCfg(kind, qbit=5, vn_cumulative=kind != 3, path=path)
+        outs, _, saved = decode(g, cfg, x, T, save=True, **kw)
+        grads = decode_backward(g, cfg, x, T, gy, list(outs), saved, **kw)
+        res[path] = (outs, grads[gi[0]], grads[gi[1]])
     assert torch.equal(res["stream"][0], res["fused"][0])
     for k in (1, 2):
         a, b = res["stream"][k].cpu().numpy(), res["fused"][k].cpu().numpy()
