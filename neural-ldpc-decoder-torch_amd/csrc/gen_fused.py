@@ -56,6 +56,7 @@ PIPE = os.environ.get("NLDPC_GEN_PIPE", "1") == "1"
 # Check-node phase: 1 = software-pipelined row copies (the LDS reads of the next row copy are issued
 # before the current one computes, so the LDS latency hides behind arithmetic instead of stalling)
 CNPIPE = os.environ.get("NLDPC_GEN_CNPIPE", "1") == "1"
+CNDEPTH = int(os.environ.get("NLDPC_GEN_CNDEPTH", "1"))  # row copies whose reads are in flight ahead (experiment)
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
 # chosen by auto_geometry
@@ -164,7 +165,8 @@ CNTID = os.environ.get("NLDPC_GEN_CNTID", "0") == "1"
 # experiment knob: the owners' v2c writes into the chunk image by ds_write_addtid_b32 as well: no address VALU
 # at all (a copy whose shifted range wraps inside the wave writes twice, each half under its own EXEC mask
 # from the scalar unit), twice the LDS store rate; same geometries as CNTID
-OWNTID = os.environ.get("NLDPC_GEN_OWNTID", "0") == "1"
+OWNTID = os.environ.get("NLDPC_GEN_OWNTID", "0") in ("1", "2", "3")
+OWNTID_MODE = int(os.environ.get("NLDPC_GEN_OWNTID", "0"))  # (debug) 2: only unwrapped copies, 3: only wrapped
 
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
 
@@ -688,7 +690,9 @@ def emit(S: Spec) -> str:
             wrap_prelude()
             for q in range(Q):
                 for k, e in mine:
-                    if OWNTID and S.ZT % 64 == 0 and not S.padded and SAVECOPY:
+                    cq_ = (q * ZT - int(S.shift[e])) % Z
+                    if OWNTID and S.ZT % 64 == 0 and not S.padded and SAVECOPY and not (
+                            OWNTID_MODE == 2 and cq_ + ZT > Z) and not (OWNTID_MODE == 3 and cq_ + ZT <= Z):
                         own_tid_write(e, q, e0, ref(p, q, k))
                         continue
                     w(f"    {own_lv(e, q, e0)} = {ref(p, q, k)};")
@@ -826,6 +830,8 @@ def emit(S: Spec) -> str:
                     if e in d1set:
                         w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = d1_v2c<KIND, {1 if ZADD else 0}>(cd[{S.cd_index[p].index((e, q))}], a); "
                           f"else m{n}[{k}] = rq{n}[{k * Z}];")
+                    elif "cnread" in SKIP:  # (timing experiment: no check-node LDS reads, junk inputs)
+                        w(f"    m{n}[{k}] = __uint_as_float(0x3f800000u + ((uint32_t)u << 8) + {k * 977 + n * 131}u);")
                     else:
                         w(f"    m{n}[{k}] = rq{n}[{k * Z}];")
 
@@ -923,7 +929,10 @@ def emit(S: Spec) -> str:
                         w(f"                y_ = posterior<KIND>(xo_, {pm}, a);")
                         w(f"                if (a.ucn) cdm = (cdm & ~(1u << {ix})) | ((y_ >= 0.f ? 1u : 0u) << {ix});")
                         w("            }")
-                        w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, y_, ps);")
+                        if "d1post" in SKIP:  # (timing experiment: no degree-1 posterior stores)
+                            w("            asm volatile(\"\" :: \"v\"(y_));")
+                        else:
+                            w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, y_, ps);")
                         w(f"            if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m{n}[{k}]);")
                         w(f"        }} else {{ rq{n}[{k * Z}] = m{n}[{k}]; }}")
                     elif "cnwrite" in SKIP:  # (timing experiment: keep the value live without the LDS write)
@@ -934,12 +943,12 @@ def emit(S: Spec) -> str:
 
             if CNPIPE:
                 # the next row copy's reads go out before this one computes (its slots are disjoint from
-                # every slot this one writes, so program order already allows it)
-                if rcs:
-                    rc_load(0)
+                # every slot this one writes, so program order already allows it); CNDEPTH row copies ahead
+                for n in range(min(CNDEPTH, len(rcs))):
+                    rc_load(n)
                 for n in range(len(rcs)):
-                    if n + 1 < len(rcs):
-                        rc_load(n + 1)
+                    if n + CNDEPTH < len(rcs):
+                        rc_load(n + CNDEPTH)
                     w("    __builtin_amdgcn_sched_barrier(0);")
                     rc_compute(n)
             else:
@@ -1457,7 +1466,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     # check nodes), and each check copy reads its row's messages from LDS at h -- no global gathers in
     # the check-node phase.  Without staging they are read from global memory at h (coalesced).
     SBY = S.stage
-    w("template <int KIND, int DC, int TIED>")
+    w("template <int KIND, int DC, int TIED, int Q0, int Q1>  // the row's copies Q0 .. Q1-1")
     w("__device__ __forceinline__ void cnb_row(float* rp, const char* sq, int u, const FusedBwdArgs& a, int it, "
       "int e0, int row, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
     w("    __builtin_amdgcn_sched_barrier(0);  // one row at a time (register pressure)")
@@ -1483,7 +1492,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w("#pragma unroll")
         w("    for (int k = 0; k < DC; ++k) gwa[k] = gba[k] = 0.f;")
     w("#pragma unroll")
-    w(f"    for (int q = 0; q < {Q}; ++q) {{")
+    w("    for (int q = Q0; q < Q1; ++q) {")
     if GWQ:  # per-copy partial sums (slot q of the wave's Q): no accumulator lives across the copies
         w("        float gwa[DC], gba[DC];")
         w("#pragma unroll")
@@ -1557,10 +1566,6 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w(f"{indent}    for (int k = 0; k < DC; ++k) t_ += gwa[k];")
         w(f"{indent}    const float s_ = wave_sum(dup_ ? 0.f : t_);")
         w(f"{indent}    if (lane0) gacc[0] += s_;")
-        w(f"{indent}    if ({last} && lane0 && a.p_cn) {{")
-        w("#pragma unroll")
-        w(f"{indent}        for (int k = 0; k < DC; ++k) a.p_cn[pc + e0 + k] = 0.f;")
-        w(f"{indent}    }}")
         w(f"{indent}}} else {{")
     if GWQ:
         tied("        ", f"q == {Q - 1}")
@@ -1580,12 +1585,22 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
               "int it, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
             w("    asm volatile(\"\" : \"+v\"(u));")
             w("    constexpr int SB = saved_msg_bytes<KIND>();")
+            # untied: whole rows per part (a row's per-edge sums add up over its copies in the wave's LDS
+            # slots); tied: (row, copy) units balanced over the parts, as the forward's check nodes
             rows = sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i]))
+            w("    if constexpr (!TIED) {")
             for i in rows:
                 es = S.row_edges[i]
                 off = (es[0] - e0c) * Z
-                w(f"    cnb_row<KIND, {len(es)}, TIED>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, svr, vcw, pc, "
-                  "lane0, dup_, gacc);")
+                w(f"        cnb_row<KIND, {len(es)}, 0, 0, {Q}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, svr, "
+                  "vcw, pc, lane0, dup_, gacc);")
+            w("    } else {")
+            for i, q in S.cn_units[ci][p]:
+                es = S.row_edges[i]
+                off = (es[0] - e0c) * Z
+                w(f"        cnb_row<KIND, {len(es)}, 1, {q}, {q + 1}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, "
+                  "svr, vcw, pc, lane0, dup_, gacc);")
+            w("    }")
             w("}")
             # the chunk's saved block -> this codeword's staging region (all threads of the workgroup)
             if SBY and p == 0:
@@ -1681,10 +1696,9 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w(f"        vnb_p{p}<KIND, TIED>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0, dup_);")
         # tied weights: the wave's sums into the part's designated entries (written 0 earlier this iteration,
         # by this wave's lane 0: program order makes these the final values)
-        rows_p = [sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i])) for ci in range(len(S.chunks))]
-        first = next((r[0] for r in rows_p if r), None)
-        if first is not None:
-            w(f"        if (TIED && a.p_cn && lane0) a.p_cn[pc + {S.row_edges[first][0]}] = gacc[0];")
+        # (the launcher zeroed the tied kernel's partials: each part's wave total goes to the part's own entry
+        # p of the row -- distinct per part, and the two waves of a part have slots of their own)
+        w(f"        if (TIED && a.p_cn && lane0) a.p_cn[pc + {p}] = gacc[0];")
 
         bstamp(1 + 3 * len(S.chunks))
         w("    }")

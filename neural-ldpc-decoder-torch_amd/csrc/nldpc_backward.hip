@@ -450,6 +450,8 @@ static int fused_backward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B,
     a.nslots = W.nslots;
     a.cn_tied = ft ? 1 : 0;
     a.vn_tied = 0;
+    // the tied kernel writes one entry per part and wave slot: the rest of its partials must read 0
+    if (ft && a.p_cn) NLDPC_HIP_CHECK(hipMemsetAsync(a.p_cn, 0, (size_t)T * W.nslots * G.E * sizeof(float), s));
     for (int k = 0; k < kFusedMaxT; ++k) a.gy.p[k] = k < T ? const_cast<float*>(grad_outs[k]) : nullptr;
     // diagnostic stamp build (lib_stamps/): NLDPC_STAMPS_BWD=<file> collects the phase stamps of each call
     static const char* stamp_file = std::getenv("NLDPC_STAMPS_BWD");

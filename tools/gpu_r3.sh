@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 for s in $PHASES; do
     echo "== $s $(date +%T)"
     case $s in
-    tests) timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -x \
+    tests) NLDPC_JIT_LOG=$O/${TAG}_jit_compiles.txt timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -x \
                -p no:cacheprovider > $O/${TAG}_gpu_tests.log 2>&1; rc=$?; tail -3 $O/${TAG}_gpu_tests.log ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1; rc=$? ;;
     cfg3)  timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $O/${TAG}_bench_cfg3.log 2>&1; rc=$?; tail -c 1500 $O/${TAG}_bench_cfg3.log ;;
