@@ -196,6 +196,15 @@ int nldpc_bce_loss(const float* const* logits, int32_t K, const float* coef, con
                    float* loss, void* work, size_t work_bytes, void* stream);
 int nldpc_bce_grad(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
                    const float* gseed, float* const* grads, void* stream);
+/* The training step's pair in one pass over the logits (read once for the loss and the gradients): the
+ * loss as nldpc_bce_loss and grads[k] as nldpc_bce_grad would write them for *gseed == 1 (what
+ * loss.backward() sends), bit for bit.  nldpc_bce_grad_unless_unit then runs at backward time with the
+ * seed that arrived: it returns at once on the device when *gseed == 1 and otherwise overwrites grads
+ * as nldpc_bce_grad does, so the pair equals nldpc_bce_loss + nldpc_bce_grad for any seed. */
+int nldpc_bce_loss_grad(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
+                        float* loss, float* const* grads, void* work, size_t work_bytes, void* stream);
+int nldpc_bce_grad_unless_unit(const float* const* logits, int32_t K, const float* coef, const float* target,
+                               int64_t n, const float* gseed, float* const* grads, void* stream);
 
 /* ---- synthetic AWGN channel (the step before the path; replaces the all-zero branch of
  *      AWGNPassedDatagen, boosted.../AWGNPassedDatagen.py:75-134, generated on the device):

@@ -139,21 +139,52 @@ __device__ __forceinline__ float bce_term_tab(float x, float t, const float (*ta
     return bce_term(x, t);
 }
 
+// GRAD: the same pass also writes every term's gradient for a unit seed (dL/dloss = 1, what
+// loss.backward() sends), grads[k][i] = (coef[k] / n) * (sigmoid(x) - t) -- bce_grad_kernel's expression
+// with *gseed = 1, so the same bits -- reading the logits once for both directions instead of twice
+// (cfg5: the separate gradient pass re-read 8.2 GB of logits and took 3.7 ms).  The sigmoid of a grid logit
+// comes from a table of the same expression, as the term does.
+__device__ __forceinline__ float bce_sig(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float bce_sig_tab(float x, const float* tab) {
+    const float k2 = x * 2.f;
+    if (k2 == rintf(k2) && fabsf(k2) <= (float)kBceGrid) return tab[(int)k2 + kBceGrid];
+    return bce_sig(x);
+}
+
+template <bool GRAD>
 __global__ __launch_bounds__(256) void bce_loss_kernel(BceArgs a, const float* __restrict__ target, int64_t n,
-                                                       double* __restrict__ part) {
+                                                       double* __restrict__ part, BceArgs g) {
     __shared__ double red[4];
     __shared__ float tab[2][2 * kBceGrid + 1];
+    __shared__ float stab[GRAD ? 2 * kBceGrid + 1 : 1];
     for (int i = threadIdx.x; i < 2 * (2 * kBceGrid + 1); i += blockDim.x) {
         const int lab = i / (2 * kBceGrid + 1), k = i % (2 * kBceGrid + 1) - kBceGrid;
         tab[lab][k + kBceGrid] = bce_term(0.5f * (float)k, (float)lab);
+        if (GRAD && lab == 0) stab[k + kBceGrid] = bce_sig(0.5f * (float)k);
     }
     __syncthreads();
+    const float scale = 1.f / (float)n;  // bce_grad_kernel's *gseed / (float)n at *gseed = 1
 #define bce_term(x, t) bce_term_tab((x), (t), tab)
+    // one term's gradient for four elements
+    auto grad4 = [&](int k, const float4& v, const float4& t, int64_t i) {
+        if constexpr (GRAD) {
+            const float c = scale * a.coef[k];
+            float4 r;
+            r.x = c * (bce_sig_tab(v.x, stab) - t.x);
+            r.y = c * (bce_sig_tab(v.y, stab) - t.y);
+            r.z = c * (bce_sig_tab(v.z, stab) - t.z);
+            r.w = c * (bce_sig_tab(v.w, stab) - t.w);
+            reinterpret_cast<float4*>(const_cast<float*>(g.x[k]))[i] = r;
+        }
+    };
     double acc0 = 0.0, acc1 = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool vec = (reinterpret_cast<uintptr_t>(target) & 15) == 0;
-    for (int k = 0; k < a.K; ++k) vec = vec && (reinterpret_cast<uintptr_t>(a.x[k]) & 15) == 0;
+    for (int k = 0; k < a.K; ++k) {
+        vec = vec && (reinterpret_cast<uintptr_t>(a.x[k]) & 15) == 0;
+        if (GRAD) vec = vec && (reinterpret_cast<uintptr_t>(g.x[k]) & 15) == 0;
+    }
     const int64_t n4 = vec ? n / 4 : 0;
     for (int64_t i = i0; i < n4; i += stride) {
         const float4 t = target ? reinterpret_cast<const float4*>(target)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -165,16 +196,23 @@ __global__ __launch_bounds__(256) void bce_loss_kernel(BceArgs a, const float* _
                                          ((double)bce_term(v.z, t.z) + (double)bce_term(v.w, t.w)));
             acc1 += (double)a.coef[k + 1] * (((double)bce_term(u.x, t.x) + (double)bce_term(u.y, t.y)) +
                                              ((double)bce_term(u.z, t.z) + (double)bce_term(u.w, t.w)));
+            grad4(k, v, t, i);
+            grad4(k + 1, u, t, i);
         }
         if (k < a.K) {
             const float4 v = reinterpret_cast<const float4*>(a.x[k])[i];
             acc0 += (double)a.coef[k] * (((double)bce_term(v.x, t.x) + (double)bce_term(v.y, t.y)) +
                                          ((double)bce_term(v.z, t.z) + (double)bce_term(v.w, t.w)));
+            grad4(k, v, t, i);
         }
     }
     for (int64_t i = 4 * n4 + i0; i < n; i += stride) {
         const float t = target ? target[i] : 0.f;
-        for (int k = 0; k < a.K; ++k) acc0 += (double)a.coef[k] * (double)bce_term(a.x[k][i], t);
+        for (int k = 0; k < a.K; ++k) {
+            const float x = a.x[k][i];
+            acc0 += (double)a.coef[k] * (double)bce_term(x, t);
+            if (GRAD) const_cast<float*>(g.x[k])[i] = (scale * a.coef[k]) * (bce_sig_tab(x, stab) - t);
+        }
     }
 #undef bce_term
     double acc = acc0 + acc1;
@@ -201,8 +239,12 @@ __global__ __launch_bounds__(64) void bce_finish_kernel(const double* __restrict
     }
 }
 
+// UNLESS_UNIT: the gradients of a unit seed are already in g (bce_loss_kernel<true>); recompute only when
+// the seed that arrived is not 1 (read on the device: no host synchronisation)
+template <bool UNLESS_UNIT>
 __global__ __launch_bounds__(256) void bce_grad_kernel(BceArgs a, const float* __restrict__ target, int64_t n,
                                                        const float* __restrict__ gseed, BceArgs g) {
+    if (UNLESS_UNIT && *gseed == 1.f) return;
     const float scale = *gseed / (float)n;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float t = target ? target[i] : 0.f;
@@ -291,15 +333,15 @@ extern "C" int nldpc_bce_loss(const float* const* logits, int32_t K, const float
             a.coef[k] = coef[k0 + k];
         }
         double* part = static_cast<double*>(work);
-        hipLaunchKernelGGL(bce_loss_kernel, dim3(nb), dim3(256), 0, s, a, target, n, part);
+        hipLaunchKernelGGL(bce_loss_kernel<false>, dim3(nb), dim3(256), 0, s, a, target, n, part, BceArgs{});
         hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(64), 0, s, part, nb, n, loss, k0 > 0 ? 1 : 0);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? NLDPC_OK : hip_fail(e, "bce_loss_kernel launch");
 }
 
-extern "C" int nldpc_bce_grad(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
-                              const float* gseed, float* const* grads, void* stream) {
+static int bce_grad(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
+                    const float* gseed, float* const* grads, void* stream, bool unless_unit) {
     if (!logits || !coef || !gseed || !grads || n <= 0 || K <= 0) return fail(NLDPC_EINVAL, "nldpc_bce_grad: bad argument");
     hipStream_t s = static_cast<hipStream_t>(stream);
     for (int k0 = 0; k0 < K; k0 += kBceMaxK) {
@@ -311,10 +353,49 @@ extern "C" int nldpc_bce_grad(const float* const* logits, int32_t K, const float
             a.coef[k] = coef[k0 + k];
             g.x[k] = grads[k0 + k];
         }
-        hipLaunchKernelGGL(bce_grad_kernel, dim3(4096), dim3(256), 0, s, a, target, n, gseed, g);
+        if (unless_unit)
+            hipLaunchKernelGGL(bce_grad_kernel<true>, dim3(4096), dim3(256), 0, s, a, target, n, gseed, g);
+        else
+            hipLaunchKernelGGL(bce_grad_kernel<false>, dim3(4096), dim3(256), 0, s, a, target, n, gseed, g);
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? NLDPC_OK : hip_fail(e, "bce_grad_kernel launch");
+}
+
+extern "C" int nldpc_bce_grad(const float* const* logits, int32_t K, const float* coef, const float* target, int64_t n,
+                              const float* gseed, float* const* grads, void* stream) {
+    return bce_grad(logits, K, coef, target, n, gseed, grads, stream, false);
+}
+
+extern "C" int nldpc_bce_grad_unless_unit(const float* const* logits, int32_t K, const float* coef, const float* target,
+                                          int64_t n, const float* gseed, float* const* grads, void* stream) {
+    return bce_grad(logits, K, coef, target, n, gseed, grads, stream, true);
+}
+
+extern "C" int nldpc_bce_loss_grad(const float* const* logits, int32_t K, const float* coef, const float* target,
+                                   int64_t n, float* loss, float* const* grads, void* work, size_t work_bytes,
+                                   void* stream) {
+    if (!logits || !coef || !loss || !grads || !work || n <= 0 || K <= 0)
+        return fail(NLDPC_EINVAL, "nldpc_bce_loss_grad: bad argument");
+    if (work_bytes < (size_t)kBceBlocks * sizeof(double))
+        return fail(NLDPC_EINVAL, "nldpc_bce_loss_grad: workspace too small");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nb = bce_blocks(n);
+    for (int k0 = 0; k0 < K; k0 += kBceMaxK) {
+        BceArgs a{}, g{};
+        a.K = g.K = K - k0 < kBceMaxK ? K - k0 : kBceMaxK;
+        for (int k = 0; k < a.K; ++k) {
+            if (!logits[k0 + k] || !grads[k0 + k]) return fail(NLDPC_EINVAL, "nldpc_bce_loss_grad: null pointer");
+            a.x[k] = logits[k0 + k];
+            a.coef[k] = coef[k0 + k];
+            g.x[k] = grads[k0 + k];
+        }
+        double* part = static_cast<double*>(work);
+        hipLaunchKernelGGL(bce_loss_kernel<true>, dim3(nb), dim3(256), 0, s, a, target, n, part, g);
+        hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(64), 0, s, part, nb, n, loss, k0 > 0 ? 1 : 0);
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NLDPC_OK : hip_fail(e, "bce_loss_kernel launch");
 }
 
 extern "C" int nldpc_awgn_llr(float* xa, int64_t B, int64_t L, float sigma, uint64_t seed, int64_t b_offset,

@@ -178,12 +178,15 @@ class BoostedNeuralLDPCDecoder(nn.Module):
                 its = self.fixed_iterative_nodes
             else:
                 its = [0]
-            for it in its:
-                for ptype, rng in ((ParamType.Weight, self.allowed_weight_range),
-                                   (ParamType.Bias, self.allowed_bias_range)):
-                    p = getattr(self, self._param_name(ptype, node_type, it), None)
-                    if p is not None:
-                        p.data.clamp_(rng.start, rng.end)
+            # one multi-tensor clamp per range instead of one kernel per parameter (cfg5: 100 launches a step);
+            # clamp_min then clamp_max is clamp_(lo, hi), element for element
+            for ptype, rng in ((ParamType.Weight, self.allowed_weight_range),
+                               (ParamType.Bias, self.allowed_bias_range)):
+                ps = [p.data for p in (getattr(self, self._param_name(ptype, node_type, it), None) for it in its)
+                      if p is not None]
+                if ps:
+                    torch._foreach_clamp_min_(ps, rng.start)
+                    torch._foreach_clamp_max_(ps, rng.end)
 
     def _get_param(self, param_type: ParamType, node_type: NodeType, iterative_node_identifier: int):
         return getattr(self, self._param_name(param_type, node_type, iterative_node_identifier), None)
@@ -276,6 +279,13 @@ class BoostedNeuralLDPCDecoder(nn.Module):
         iteration (Boosted…py:114-124)."""
         return self.node_weight_sharing_config.get(node_type) == 3
 
+    def _tied_rows(self, node_type, run, width):
+        """[len(run), width] rows of one weight each (sharing code 3) as ONE expand of the stacked scalars:
+        the same values as stacking the per-iteration expands, but autograd reduces all rows' gradients
+        in one kernel instead of one reduction per parameter (cfg5: 100 launches a step)."""
+        ps = [self.fetch_param(ParamType.Weight, node_type, t).to(torch.float32).reshape(1) for t in run]
+        return torch.stack(ps).expand(len(run), width)
+
     @torch.no_grad()
     def count_errors(self, xa, y=None, convention=0):
         """Count-only decode (extension): int64 [T, 2] device tensor of (bit errors, frame
@@ -363,12 +373,18 @@ class BoostedNeuralLDPCDecoder(nn.Module):
                             keep_state=not last, cn_tied=self._tied(NodeType.CN))
             stack = lambda ws: torch.stack(ws) if ws[0] is not None else None  # noqa: E731
             w_vn_all = torch.stack(prefix + w_vn) if has_vn else None
+            if self._tied(NodeType.VN) and has_vn and not prefix:
+                w_vn_all = self._tied_rows(NodeType.VN, run, self.N)
             app_prev = None
             if cfg.ucn and run[0] > 0:
                 app_prev = self.outputs[run[0] - 1].reshape(self.batch_size, self.N * self.Z).detach()
             # the state this run starts from: this call's own (differentiable) or a stored one (:343, :377)
             state_in = live[run[0]] if run[0] in live else self._state(run[0])
             wc, wu = stack(w_cn), stack(w_ucn)
+            if self._tied(NodeType.CN) and wc is not None:
+                wc = self._tied_rows(NodeType.CN, run, int(self.sum_edge))
+                if wu is not None:
+                    wu = self._tied_rows(NodeType.UCN, run, int(self.sum_edge))
             # the entries this run rewrites let go of the previous call's outputs first (the list is refilled
             # below, as the reference's :523 overwrites it): otherwise two T x [B, N*Z] buffers are alive at
             # once (cfg3: 2 x 105 GB); a caller holding those tensors keeps them regardless

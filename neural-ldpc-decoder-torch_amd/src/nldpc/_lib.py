@@ -28,8 +28,12 @@ EXPORTED = (
     "nldpc_abi_version", "nldpc_last_error", "nldpc_graph_create", "nldpc_graph_destroy", "nldpc_graph_dims",
     "nldpc_graph_edges", "nldpc_graph_attach_kernel", "nldpc_graph_kernels", "nldpc_fast_path", "nldpc_saved_bytes", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
     "nldpc_awgn_llr", "nldpc_profile_begin", "nldpc_profile_end", "nldpc_bce_workspace", "nldpc_bce_loss",
-    "nldpc_bce_grad", "nldpc_forward_count", "nldpc_channel_llr", "nldpc_hbm_probe",
+    "nldpc_bce_grad", "nldpc_bce_loss_grad", "nldpc_bce_grad_unless_unit", "nldpc_forward_count", "nldpc_channel_llr", "nldpc_hbm_probe",
 )
+
+
+# entries added after the ABI 4 structs were fixed (no layout change): optional in older builds
+_ADDED_IN_ABI4 = ("nldpc_bce_loss_grad", "nldpc_bce_grad_unless_unit")
 
 
 class NldpcCfg(ctypes.Structure):
@@ -93,8 +97,13 @@ def _declare(lib):
         "nldpc_bce_workspace": (_i32, [_i64, _i32, ctypes.POINTER(ctypes.c_size_t)]),
         "nldpc_bce_loss": (_i32, [_PP, _i32, ctypes.POINTER(ctypes.c_float), _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
         "nldpc_bce_grad": (_i32, [_PP, _i32, ctypes.POINTER(ctypes.c_float), _vp, _i64, _vp, _PP, _vp]),
+        "nldpc_bce_loss_grad": (_i32, [_PP, _i32, ctypes.POINTER(ctypes.c_float), _vp, _i64, _vp, _PP, _vp,
+                                       ctypes.c_size_t, _vp]),
+        "nldpc_bce_grad_unless_unit": (_i32, [_PP, _i32, ctypes.POINTER(ctypes.c_float), _vp, _i64, _vp, _PP, _vp]),
     }
     for name, (res, args) in sig.items():
+        if name in _ADDED_IN_ABI4 and not hasattr(lib, name):
+            continue  # an experiment library built before these entries (tools/exp_build.sh): the old pair runs
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -12,7 +12,12 @@ from . import _lib
 
 
 class BCEMultiFn(torch.autograd.Function):
-    """loss = sum_k coef[k] * mean(bce_with_logits(outputs[k], target)); coef already normalised."""
+    """loss = sum_k coef[k] * mean(bce_with_logits(outputs[k], target)); coef already normalised.
+
+    When an output needs a gradient, the forward pass also writes every output's gradient for a unit seed
+    (nldpc_bce_loss_grad: the logits are read once for both directions), and backward returns those,
+    recomputed on the device only if the seed that arrives is not 1 (nldpc_bce_grad_unless_unit) -- the
+    same values as the separate gradient pass for any seed."""
 
     @staticmethod
     def forward(ctx, target, coef, *outputs):
@@ -28,10 +33,20 @@ class BCEMultiFn(torch.autograd.Function):
         work = torch.empty((int(nb.value),), dtype=torch.uint8, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         px, keep = _lib.ptr_array(xs)
-        st = L.nldpc_bce_loss(px, K, c, _lib.ptr(t), n, _lib.ptr(loss), _lib.ptr(work), int(work.numel()),
-                              _lib.stream_of(dev))
+        ctx.grads = None
+        if any(ctx.needs_input_grad[2:]) and hasattr(L, "nldpc_bce_loss_grad"):
+            grads = [torch.empty_like(x) for x in xs]
+            pg, keep_g = _lib.ptr_array(grads)
+            st = L.nldpc_bce_loss_grad(px, K, c, _lib.ptr(t), n, _lib.ptr(loss), pg, _lib.ptr(work),
+                                       int(work.numel()), _lib.stream_of(dev))
+            del keep_g
+            _lib.check(st, "nldpc_bce_loss_grad")
+            ctx.grads = grads
+        else:
+            st = L.nldpc_bce_loss(px, K, c, _lib.ptr(t), n, _lib.ptr(loss), _lib.ptr(work), int(work.numel()),
+                                  _lib.stream_of(dev))
+            _lib.check(st, "nldpc_bce_loss")
         del keep
-        _lib.check(st, "nldpc_bce_loss")
         ctx.coef = [float(v) for v in coef]
         ctx.save_for_backward(t, *xs)
         return loss
@@ -42,12 +57,15 @@ class BCEMultiFn(torch.autograd.Function):
         L = _lib.lib()
         dev = xs[0].device
         K, n = len(xs), xs[0].numel()
-        grads = [torch.empty_like(x) for x in xs]
+        grads, ctx.grads = ctx.grads, None  # (a second backward through a retained graph recomputes them)
+        entry = L.nldpc_bce_grad_unless_unit if grads is not None else L.nldpc_bce_grad
+        if grads is None:
+            grads = [torch.empty_like(x) for x in xs]
         c = (ctypes.c_float * K)(*ctx.coef)
         gs = g.detach().to(torch.float32).reshape(()).contiguous()
         px, k1 = _lib.ptr_array(xs)
         pg, k2 = _lib.ptr_array(grads)
-        st = L.nldpc_bce_grad(px, K, c, _lib.ptr(t), n, _lib.ptr(gs), pg, _lib.stream_of(dev))
+        st = entry(px, K, c, _lib.ptr(t), n, _lib.ptr(gs), pg, _lib.stream_of(dev))
         del k1, k2
         _lib.check(st, "nldpc_bce_grad")
         return (None, None, *grads)

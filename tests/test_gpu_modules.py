@@ -272,6 +272,47 @@ def test_bce_multi_matches_torch(K, etha):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed_scale", [1.0, 3.0])
+def test_bce_loss_grad_one_pass_equals_two_passes(seed_scale):
+    """The training path's single pass (nldpc_bce_loss_grad: loss + unit-seed gradients) and the backward's
+    nldpc_bce_grad_unless_unit give the gradients of the two-pass form (nldpc_bce_loss, then
+    nldpc_bce_grad with the seed that arrives) bit for bit -- with loss.backward()'s unit seed and with a
+    scaled one, which the second call recomputes on the device; grid logits (the table) and off-grid ones,
+    an odd length (the scalar tail)."""
+    from nldpc import _lib
+    from nldpc.loss import bce_multi
+    import ctypes
+    g = torch.Generator().manual_seed(11)
+    K, n = 5, 4 * 3001 + 3
+    xs = [(torch.randint(-40, 41, (n,), generator=g).float() * 0.5) for _ in range(K)]
+    xs[1][::7] += 0.37
+    y = (torch.rand(n, generator=g) < 0.4).float().to(DEV)
+    coef = [0.1, 0.2, 0.3, 0.15, 0.25]
+    outs = [x.to(DEV).requires_grad_() for x in xs]
+    loss = bce_multi(outs, y, coef)
+    (seed_scale * loss).backward()
+    # the two-pass form through the C ABI
+    L = _lib.lib()
+    dx = [x.to(DEV) for x in xs]
+    c = (ctypes.c_float * K)(*coef)
+    nb = ctypes.c_size_t(0)
+    _lib.check(L.nldpc_bce_workspace(n, K, ctypes.byref(nb)))
+    work = torch.empty((int(nb.value),), dtype=torch.uint8, device=DEV)
+    ref_loss = torch.empty((), dtype=torch.float32, device=DEV)
+    px, k1 = _lib.ptr_array(dx)
+    _lib.check(L.nldpc_bce_loss(px, K, c, _lib.ptr(y), n, _lib.ptr(ref_loss), _lib.ptr(work), int(work.numel()),
+                                _lib.stream_of(DEV)))
+    grads = [torch.empty_like(x) for x in dx]
+    gs = torch.tensor(seed_scale, dtype=torch.float32, device=DEV)
+    pg, k2 = _lib.ptr_array(grads)
+    _lib.check(L.nldpc_bce_grad(px, K, c, _lib.ptr(y), n, _lib.ptr(gs), pg, _lib.stream_of(DEV)))
+    torch.cuda.synchronize()
+    assert loss.item() == ref_loss.item()
+    for o, r in zip(outs, grads):
+        assert torch.equal(o.grad.view(torch.int32), r.view(torch.int32))
+
+
+@pytest.mark.gpu
 def test_bce_loss_grid_table_path():
     """The loss pass takes half-integer logits with 0/1 labels (every QMS decoder output) from a table of
     the same term function (nldpc_aux.hip bce_term_tab): grid logits, off-grid logits, logits past the
