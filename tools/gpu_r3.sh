@@ -38,6 +38,10 @@ for s in $PHASES; do
     stampsucn) NLDPC_LIB_PATH=$R/neural-ldpc-decoder-torch_amd/lib_stamps/libnldpc.so NLDPC_STAMPS=$O/${TAG}_stamps_ucn.bin \
              timeout -k 10 300 python -u bench.py --workload cfg3ucn --steps 1 --warmup 1 --batch 16384 --no-profile --no-cpu-baseline > $O/${TAG}_stamps_ucn_bench.log 2>&1 &&
            python3 tools/stamps2.py $O/${TAG}_stamps_ucn.bin > $O/${TAG}_stamps_ucn.txt 2>&1; rc=$?; head -30 $O/${TAG}_stamps_ucn.txt ;;
+    stamps3|stamps2) W=cfg3; BA="--batch 16384"; [ $s = stamps2 ] && { W=cfg2; BA=""; }
+           NLDPC_LIB_PATH=$R/neural-ldpc-decoder-torch_amd/lib_stamps/libnldpc.so NLDPC_STAMPS=$O/${TAG}_$s.bin \
+             timeout -k 10 300 python -u bench.py --workload $W --steps 1 --warmup 1 $BA --no-profile --no-cpu-baseline --no-sweep --no-count-only > $O/${TAG}_${s}_bench.log 2>&1 &&
+           python3 tools/stamps2.py $O/${TAG}_$s.bin > $O/${TAG}_$s.txt 2>&1; rc=$?; head -30 $O/${TAG}_$s.txt ;;
     abq)   for v in ${VARIANTS}; do
                NLDPC_LIB_PATH=$R/neural-ldpc-decoder-torch_amd/lib_exp/$v/libnldpc.so timeout -k 10 300 python -u bench.py --workload ${WL:-cfg3ucn} ${BENCH_ARGS} \
                    --steps ${NSTEPS:-4} --warmup 2 --no-cpu-baseline > $O/${TAG}_abq_$v.log 2>&1 || { echo "$v failed"; tail -5 $O/${TAG}_abq_$v.log; exit 1; }
