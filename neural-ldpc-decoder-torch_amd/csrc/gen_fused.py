@@ -155,6 +155,10 @@ D1B = os.environ.get("NLDPC_GEN_D1B", "1") == "1"
 # the tied-CN-weight backward kernels (MODE 5, default 1); experiment builds: NLDPC_GEN_TIED=0 leaves them out,
 # NLDPC_GEN_NOBWD=1 every backward kernel (decode-only A/B libraries compile in a fraction of the time)
 TIED_BWD = os.environ.get("NLDPC_GEN_TIED", "1") == "1"
+# the tied kernel's check-node work as (row, lane copy) units balanced over the parts (1) or as whole rows
+# per part like the untied kernel (0, default): cfg5 backward 28.33 vs 27.87 ms, step 46.09 vs 45.65 ms
+# (same box, profiles/r4c_ab_cfg5.txt) -- the units form spilled more (139 VGPRs against 66)
+TIED_UNITS = os.environ.get("NLDPC_GEN_TIEDUNITS", "0") == "1"
 NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"
 
 # experiment knob: check-node writes (c2v back into the chunk image) by ds_write_addtid_b32 -- address = M0 +
@@ -1585,8 +1589,9 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
               "int it, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
             w("    asm volatile(\"\" : \"+v\"(u));")
             w("    constexpr int SB = saved_msg_bytes<KIND>();")
-            # untied: whole rows per part (a row's per-edge sums add up over its copies in the wave's LDS
-            # slots); tied: (row, copy) units balanced over the parts, as the forward's check nodes
+            # whole rows per part (untied: a row's per-edge sums add up over its copies in the wave's LDS
+            # slots; tied: one wave sum per row copy); NLDPC_GEN_TIEDUNITS=1: the tied kernel by (row, copy)
+            # units balanced over the parts, as the forward's check nodes
             rows = sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i]))
             w("    if constexpr (!TIED) {")
             for i in rows:
@@ -1595,10 +1600,11 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 w(f"        cnb_row<KIND, {len(es)}, 0, 0, {Q}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, svr, "
                   "vcw, pc, lane0, dup_, gacc);")
             w("    } else {")
-            for i, q in S.cn_units[ci][p]:
+            for i, q in (S.cn_units[ci][p] if TIED_UNITS else [(i, None) for i in rows]):
                 es = S.row_edges[i]
                 off = (es[0] - e0c) * Z
-                w(f"        cnb_row<KIND, {len(es)}, 1, {q}, {q + 1}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, "
+                q0, q1 = (q, q + 1) if q is not None else (0, Q)
+                w(f"        cnb_row<KIND, {len(es)}, 1, {q0}, {q1}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, "
                   "svr, vcw, pc, lane0, dup_, gacc);")
             w("    }")
             w("}")

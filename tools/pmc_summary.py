@@ -44,7 +44,9 @@ out["calibration"] = {
     "fetch_ratio_16B": fv[2] * 1024 / gib, "fetch_ratio_4B": fv[3] * 1024 / gib, "write_ratio": wv[1] * 1024 / gib,
 }
 KERNELS = {"cfg3": [("fused", "fused_bg2_z384::kernel<3, 0>", 65536)],
-           "cfg5": [("fused", "fused_bg2_z384::kernel<2, 1>", 2048), ("fusedb", "_bg2_z384::bwd_kernel<2>", 2048)],
+           "cfg2": [("fused", "fused_wimax_z24::kernel<3, 0>", 4096)],
+           # (the backward's template is <KIND, TIED> since r4: the prefix matches both)
+           "cfg5": [("fused", "fused_bg2_z384::kernel<2, 1>", 2048), ("fusedb", "_bg2_z384::bwd_kernel<2", 2048)],
            "cfg3ucn": [("fused", "fused_bg2_z384::kernel<1, 0>", 65536)]}
 # Boosted side lines, one entry per (kind, sharing codes): bench.py --workload cfg3ucn --kind K --nw a,b,c
 for _k, _kind in (("MS", 1), ("QMS", 2), ("SP", 0)):
