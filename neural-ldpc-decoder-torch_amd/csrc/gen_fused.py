@@ -63,7 +63,7 @@ CNDEPTH = int(os.environ.get("NLDPC_GEN_CNDEPTH", "1"))  # row copies whose read
 SPECS = [
     ("bg2_z384", "basegraph2_set0.txt", 384, 1, 8, 3),
     ("bg2_z16", "basegraph2_set0.txt", 16, 16, 2, 1),
-    ("wimax_z24", "wman_N0576_R34_z24.txt", 24, 16, 1, 1),
+    ("wimax_z24", "wman_N0576_R34_z24.txt", 24, 8, 4, 1),  # r4: 0.160 -> 0.114 ms at cfg2 (profiles/r4_ab.txt)
     ("bg2_z96", "basegraph2_set0.txt", 96, None, None, None),
 ]
 # More (graph, Z) pairs at build time: NLDPC_FUSED_EXTRA="bg2:192,wimax:48,<file.txt>:Z" (base graph
@@ -155,6 +155,12 @@ D1B = os.environ.get("NLDPC_GEN_D1B", "1") == "1"
 # the tied-CN-weight backward kernels (MODE 5, default 1); experiment builds: NLDPC_GEN_TIED=0 leaves them out,
 # NLDPC_GEN_NOBWD=1 every backward kernel (decode-only A/B libraries compile in a fraction of the time)
 TIED_BWD = os.environ.get("NLDPC_GEN_TIED", "1") == "1"
+# Neural decode, pipelined schedule with >= 3 chunks: the VN sums over a column's edges in chunks 0-1 run
+# right after those messages are read back (the [W2, R1] phase, which has LDS traffic and no check-node
+# work), the rest in the VN phase.  Exact: the reference's left fold S_k = ((P_{k-1} + c_{k+1}) + ...)
+# splits at any edge; E_k (the fold up to the last early edge) replaces c_k in its register, which no
+# later sum reads, and the prefix P_{m-1} waits in one register per column copy.
+EARLYVN = os.environ.get("NLDPC_GEN_EARLYVN", "0") == "1"
 # the tied kernel's check-node work as (row, lane copy) units balanced over the parts (1) or as whole rows
 # per part like the untied kernel (0, default): cfg5 backward 28.33 vs 27.87 ms, step 46.09 vs 45.65 ms
 # (same box, profiles/r4c_ab_cfg5.txt) -- the units form spilled more (139 VGPRs against 66)
@@ -395,6 +401,8 @@ def emit(S: Spec) -> str:
     w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
     d1b = D1B and not S.ucn_wave  # (the window-XOR UCN check side reads the degree-1 columns' LDS words)
     w(f"#define D1_BYPASS ((KIND == NLDPC_NEURAL{' || KIND == NLDPC_MS || KIND == NLDPC_QMS' if d1b else ''}) && !SAVE)")
+    w(f"#define EARLY_VN ({'KIND == NLDPC_NEURAL && !SAVE' if EARLYVN and S.pipe and len(S.chunks) >= 3 else 'false'})"
+      "  // VN sums split around the [W2, R1] phase (EARLYVN)")
     w("// check-row LDS addresses from one 32-bit base (ROADDR); in the QMS / SP kernels it measured slower")
     w("#define ROA (KIND == NLDPC_NEURAL || KIND == NLDPC_MS)")
     w(f"#define UCNW ((KIND == NLDPC_MS{' || KIND == NLDPC_QMS' if UCNW_QMS else ''}) && {'true' if S.ucn_wave else 'false'})  "
@@ -412,6 +420,19 @@ def emit(S: Spec) -> str:
 
     def NS(p):
         return Q - 2 * NP(p)
+
+    # EARLYVN (see the knob): the early VN sums cover each column's edges below the end of chunk 1
+    EVN = EARLYVN and S.pipe and len(S.chunks) >= 3 and all(NP(p_) == 0 for p_ in range(S.P))
+    esplit = S.chunks[1][3] if EVN else 0
+
+    def early_m(j):  # the column's edges in chunks 0-1 (its edges are in row order)
+        return sum(1 for e in S.col_edges[j] if e < esplit) if EVN else 0
+
+    def pe_params(p):  # the prefix P_{m-1} of each register column and lane copy, between the two parts
+        return "".join(f", float (&pe{i})[{max(len(S.reg_cols[p]), 1)}]" for i in range(NS(p))) if EVN else ""
+
+    def pe_args(p):
+        return "".join(f", pe{i}" for i in range(NS(p))) if EVN else ""
 
     def ref(p, q, k):
         if q < 2 * NP(p):
@@ -453,7 +474,7 @@ def emit(S: Spec) -> str:
     def X(j, q):  # byte offset of variable copy (column j, lane copy q) in a [N][Z] codeword
         return 4 * (j * Z + q * ZT)
 
-    def vn_col(p, n, j, s, d, final):
+    def vn_col(p, n, j, s, d, final, early=False):
         """VN (or final posterior) of column j (n-th register column of part p) for every copy group of
         the lane at once: the packed-pair chains (v_pk_add_f32, copies 2i/2i+1) and the scalar chain
         (last copy) are emitted interleaved, so consecutive adds never depend on each other (gfx950
@@ -499,40 +520,74 @@ def emit(S: Spec) -> str:
             # edges two at a time: the chains of k and k+1 (S_k from P_{k-1}, S_{k+1} from P_k) run
             # interleaved -- twice the independent adds per wave for the VN's dependent-add tail.
             # Chain k reads c_{k+1} first, before chain k+1 overwrites it with v2c_{k+1}.
-            for k in range(0, d, 2):
-                two = k + 1 < d
-                w("            {")
-                if two:
-                    for T_, arr, xin, g in grp:
-                        pk = f"{arr}[{s + k}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k}]')
-                        w(f"                const {T_} Pk_{g} = {pk};  // P_k")
-                    for T_, arr, xin, g in grp:
-                        s1 = f"{arr}[{s + k + 1}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k + 1}]')
-                        w(f"                {T_} S_{g} = {s1};")
-                        w(f"                {T_} U_{g} = Pk_{g};")
-                    for m in range(k + 2, d):
+            def pairs(k_from, d_, out, ind="            "):
+                """Chains k_from .. d_-1 over c_{k+1} .. c_{d_-1} from the running prefix P; out(g, v) forms
+                what a chain's register receives (v2c = x0 + S, or the partial sum itself)."""
+                for k in range(k_from, d_, 2):
+                    two = k + 1 < d_
+                    w(f"{ind}{{")
+                    if two:
                         for T_, arr, xin, g in grp:
-                            w(f"                S_{g} = {add(T_, f'S_{g}', f'{arr}[{s + m}]')};")
-                            w(f"                U_{g} = {add(T_, f'U_{g}', f'{arr}[{s + m}]')};")
+                            pk = f"{arr}[{s + k}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k}]')
+                            w(f"{ind}    const {T_} Pk_{g} = {pk};  // P_k")
+                        for T_, arr, xin, g in grp:
+                            s1 = f"{arr}[{s + k + 1}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k + 1}]')
+                            w(f"{ind}    {T_} S_{g} = {s1};")
+                            w(f"{ind}    {T_} U_{g} = Pk_{g};")
+                        for m in range(k + 2, d_):
+                            for T_, arr, xin, g in grp:
+                                w(f"{ind}    S_{g} = {add(T_, f'S_{g}', f'{arr}[{s + m}]')};")
+                                w(f"{ind}    U_{g} = {add(T_, f'U_{g}', f'{arr}[{s + m}]')};")
+                        for T_, arr, xin, g in grp:
+                            w(f"{ind}    const {T_} o_{g} = {arr}[{s + k + 1}];")
+                            w(f"{ind}    {arr}[{s + k}] = {out(T_, g, f'S_{g}')}; "
+                              f"{arr}[{s + k + 1}] = {out(T_, g, f'U_{g}')};")
+                        # the fake dependence of the running prefix on the new messages keeps the compiler
+                        # from running the prefix chain ahead and holding every partial sum in a register
+                        for T_, arr, xin, g in grp:
+                            w(f"{ind}    asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]), \"v\"({arr}[{s + k + 1}]));")
+                        for T_, arr, xin, g in grp:
+                            w(f"{ind}    P_{g} = {add(T_, f'Pk_{g}', f'o_{g}')};")
+                    else:
+                        for T_, arr, xin, g in grp:
+                            w(f"{ind}    {T_} S_{g} = P_{g};")
+                        for T_, arr, xin, g in grp:
+                            w(f"{ind}    const {T_} o_{g} = {arr}[{s + k}]; {arr}[{s + k}] = {out(T_, g, f'S_{g}')};")
+                        for T_, arr, xin, g in grp:
+                            w(f"{ind}    asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]));")
+                        for T_, arr, xin, g in grp:
+                            w(f"{ind}    P_{g} = {add(T_, f'P_{g}', f'o_{g}')};")
+                    w(f"{ind}}}")
+
+            v2c = lambda T_, g, v: add(T_, f"x0_{g}", v)  # noqa: E731
+            m_ = early_m(j)
+            if early:
+                w("            if constexpr (EARLY_VN) {")
+                # EARLYVN late part: chains k < m continue from E_k (their registers) over c_m .. c_{d-1} --
+                # all of them before the chains k >= m overwrite c_m ..; then the prefix continues from P_{m-1}
+                for k in range(0, m_, 2):
+                    two = k + 1 < m_
+                    w("                {")
                     for T_, arr, xin, g in grp:
-                        w(f"                const {T_} o_{g} = {arr}[{s + k + 1}];")
-                        w(f"                {arr}[{s + k}] = {add(T_, f'x0_{g}', f'S_{g}')}; "
-                          f"{arr}[{s + k + 1}] = {add(T_, f'x0_{g}', f'U_{g}')};")
-                    # the fake dependence of the running prefix on the new messages keeps the compiler
-                    # from running the prefix chain ahead and holding every partial sum in a register
+                        w(f"                    {T_} S_{g} = {arr}[{s + k}];")
+                        if two:
+                            w(f"                    {T_} U_{g} = {arr}[{s + k + 1}];")
+                    for m in range(m_, d):
+                        for T_, arr, xin, g in grp:
+                            w(f"                    S_{g} = {add(T_, f'S_{g}', f'{arr}[{s + m}]')};")
+                            if two:
+                                w(f"                    U_{g} = {add(T_, f'U_{g}', f'{arr}[{s + m}]')};")
                     for T_, arr, xin, g in grp:
-                        w(f"                asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]), \"v\"({arr}[{s + k + 1}]));")
-                    for T_, arr, xin, g in grp:
-                        w(f"                P_{g} = {add(T_, f'Pk_{g}', f'o_{g}')};")
-                else:
-                    for T_, arr, xin, g in grp:
-                        w(f"                {T_} S_{g} = P_{g};")
-                    for T_, arr, xin, g in grp:
-                        w(f"                const {T_} o_{g} = {arr}[{s + k}]; {arr}[{s + k}] = {add(T_, f'x0_{g}', f'S_{g}')};")
-                    for T_, arr, xin, g in grp:
-                        w(f"                asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]));")
-                    for T_, arr, xin, g in grp:
-                        w(f"                P_{g} = {add(T_, f'P_{g}', f'o_{g}')};")
+                        w(f"                    {arr}[{s + k}] = {v2c(T_, g, f'S_{g}')};")
+                        if two:
+                            w(f"                    {arr}[{s + k + 1}] = {v2c(T_, g, f'U_{g}')};")
+                    w("                }")
+                for T_, arr, xin, g in grp:
+                    w(f"                P_{g} = pe{g[1:]}[{n}];")
+                pairs(m_, d, v2c, "                ")
+                w("            } else {")
+            pairs(0, d, v2c)
+            if early:
                 w("            }")
             if QEXACT:
                 w("            }")
@@ -549,7 +604,7 @@ def emit(S: Spec) -> str:
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void {fname}({state_params(p)}, {x_params(p)}, const FusedArgs& a, "
               f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t* appw, int u, "
-              f"uint32_t d1m, rsrc_t apr) {{")
+              f"uint32_t d1m, rsrc_t apr{pe_params(p)}) {{")
             if not final:
                 w("    const bool ucn_ = KIND != NLDPC_NEURAL && a.ucn;  // UCN: hard decisions of the previous posterior")
             if XPRE2 and NP(p) == 0:
@@ -561,7 +616,7 @@ def emit(S: Spec) -> str:
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
-                vn_col(p, n, j, s, d, final)
+                vn_col(p, n, j, s, d, final, early=not final and early_m(j) >= 2)
                 for i in range(NP(p)):
                     w("            {")
                     if XPRE:
@@ -627,6 +682,57 @@ def emit(S: Spec) -> str:
                         else:
                             w(f"        app_or(appw, {j * S.WZX}, u + {q * ZT}, {bit});")
                 w("    }")
+            w("}")
+
+    # EARLYVN early part: for each column's edges k < m (chunks 0-1), E_k = ((P_{k-1} + c_{k+1}) + ...) + c_{m-1}
+    # replaces c_k (read by no later sum), the prefix P_{m-1} goes to pe -- the same operations, in the same
+    # order, as the first steps of vn_col's chains (pairs of chains interleaved as there)
+    if EVN:
+        for p in range(S.P):
+            w("template <int KIND, int MODE>")
+            w(f"__device__ __forceinline__ void vne_p{p}({state_params(p)}{pe_params(p)}) {{")
+            s_ = 0
+            for n, j in enumerate(S.reg_cols[p]):
+                d, m_ = len(S.col_edges[j]), early_m(j)
+                if m_ >= 2:
+                    gs = [(f"cs{i}", f"s{i}", i) for i in range(NS(p))]
+                    w(f"    {{  // column {j}: edges 0..{m_ - 1} of {d}")
+                    for arr, g, i in gs:
+                        w(f"        float P_{g} = 0.f;")
+                    for k in range(0, m_, 2):
+                        two = k + 1 < m_
+                        w("        {")
+                        if two:
+                            for arr, g, i in gs:
+                                pk = f"{arr}[{s_ + k}]" if k == 0 and not ZADD else f"fadd(P_{g}, {arr}[{s_ + k}])"
+                                w(f"            const float Pk_{g} = {pk};")
+                            for arr, g, i in gs:
+                                s1 = f"{arr}[{s_ + k + 1}]" if k == 0 and not ZADD else f"fadd(P_{g}, {arr}[{s_ + k + 1}])"
+                                w(f"            float S_{g} = {s1};")
+                                w(f"            float U_{g} = Pk_{g};")
+                            for mm in range(k + 2, m_):
+                                for arr, g, i in gs:
+                                    w(f"            S_{g} = fadd(S_{g}, {arr}[{s_ + mm}]);")
+                                    w(f"            U_{g} = fadd(U_{g}, {arr}[{s_ + mm}]);")
+                            for arr, g, i in gs:
+                                w(f"            const float o_{g} = {arr}[{s_ + k + 1}];")
+                                w(f"            {arr}[{s_ + k}] = S_{g}; {arr}[{s_ + k + 1}] = U_{g};")
+                            for arr, g, i in gs:
+                                w(f"            asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s_ + k}]), \"v\"({arr}[{s_ + k + 1}]));")
+                            for arr, g, i in gs:
+                                w(f"            P_{g} = fadd(Pk_{g}, o_{g});")
+                        else:
+                            for arr, g, i in gs:
+                                w(f"            const float o_{g} = {arr}[{s_ + k}]; {arr}[{s_ + k}] = P_{g};")
+                            for arr, g, i in gs:
+                                w(f"            asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s_ + k}]));")
+                            for arr, g, i in gs:
+                                w(f"            P_{g} = fadd(P_{g}, o_{g});")
+                        w("        }")
+                    for arr, g, i in gs:
+                        w(f"        pe{i}[{n}] = P_{g};")
+                    w("    }")
+                s_ += d
             w("}")
 
     # ---------------------------------------------------------------- LDS chunk write / read-back
@@ -1077,6 +1183,9 @@ def emit(S: Spec) -> str:
         for i in range(NS(p)):
             w(f"    float cs{i}[{sp}], xs{i}[{nr}];")
         w(f"    float xd[{nd}];")
+        if EVN:
+            for i in range(NS(p)):
+                w(f"    float pe{i}[{nr}];  // EARLYVN: the prefix of the early edges, column by column")
         w("#pragma unroll")
         w(f"    for (int k = 0; k < {sp}; ++k) {{")
         for i in range(NP(p)):
@@ -1147,6 +1256,8 @@ def emit(S: Spec) -> str:
         w(f"        for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
         w("        __syncthreads();")
         w("    }")
+        if EVN:  # the all-zero starting state's early sums (the first VN continues them)
+            w(f"    if constexpr (EARLY_VN) vne_p{p}<KIND, MODE>({state_args(p)}{pe_args(p)});")
         w("    for (int it = 0; it < a.T; ++it) {")
         stamp(0)
         w("        if (KIND != NLDPC_NEURAL && a.w_vn) {")
@@ -1168,7 +1279,7 @@ def emit(S: Spec) -> str:
         w(f"        const rsrc_t pm = make_rsrc((const float*)(pmp ? pmp + blk * {NZ} : nullptr), pmp ? nlive * {NZ} : 0);")
         setprio(p, 0)
         if "vn" not in SKIP:
-            w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
+            w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr{pe_args(p)});")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
         w(f"        if constexpr (CNT) {{ if (dup_) ps.ec = 0; if (it >= 1) ps.{cnt_flush}({cnt_slot}, it - 1); else ps.ec = 0; }}")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
@@ -1253,6 +1364,8 @@ def emit(S: Spec) -> str:
                     setprio(p, 0)  # [R_{K-1}] belongs to the next VN phase
                 for kind_, ci in ph:
                     {"w": op_w, "cn": op_cn, "r": op_r}[kind_](ci)
+                    if EVN and kind_ == "r" and ci == 1:  # chunks 0-1 are back: the next VN's early sums
+                        w(f"        if constexpr (EARLY_VN) {{ if (it + 1 < a.T) vne_p{p}<KIND, MODE>({state_args(p)}{pe_args(p)}); }}")
                 stamp(2 + k)  # arrival at the barrier that ends phase k (stamp 1: after the VN)
                 if k < len(phases) - 1:
                     # (timing experiment SKIP=sync: no barrier -- racy results, the cost of waiting at them)
@@ -1268,7 +1381,7 @@ def emit(S: Spec) -> str:
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
         w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
-        w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr);")
+        w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr{pe_args(p)});")
         w(f"    if constexpr (CNT) {{ if (dup_) ps.ec = 0; ps.{cnt_flush}({cnt_slot}, a.T - 1); }}")
         w("    if (a.c2v_out) {")
         for q in range(Q):
