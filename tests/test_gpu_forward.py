@@ -508,6 +508,36 @@ def test_runtime_kernel_training_step_matches_streaming(kind, Z, B):
         np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-5 * np.abs(a).max())
 
 
+@pytest.mark.parametrize("kind", [1, 2])
+def test_tied_cn_backward_row_sums_match_untied(kind):
+    """NLDPC_FLAG_CN_TIED (sharing code 3: one CN weight per iteration, expanded to [T][E]): the fused
+    backward's tied kernel reduces each row copy once and spreads the iteration's total over a few entries;
+    every iteration's row sum must equal the untied kernel's (per-edge gradients summed), and the other
+    weight gradient (VN) must be the same (BG2 z=16, built in; z=384 through the cfg5 module test)."""
+    from nldpc.decode import DecodeCfg, decode, decode_backward
+    from oracle.ldpc_oracle import quantize
+    T, B, Z = 5, 3, 16
+    g = _graph(BG2, Z)
+    gen = torch.Generator().manual_seed(30 + kind)
+    x = (2 * (-1 + 0.85 * torch.randn(B, 52, Z, generator=gen)) / 0.7225).float()
+    if kind == 2:
+        x = quantize(x, 5)
+    x = x.to(DEV)
+    wc = (0.5 + torch.rand(T, 1, generator=gen)).expand(T, g.E).contiguous().to(DEV)
+    wv = (0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV)
+    gy = [torch.randn(B, 52 * Z, generator=gen).to(DEV) for _ in range(T)]
+    res = {}
+    for tied in (False, True):
+        cfg = DecodeCfg(kind, qbit=5, vn_cumulative=True, path="fused", cn_tied=tied)
+        outs, _, saved = decode(g, cfg, x, T, save=True, w_cn=wc, w_vn=wv)
+        g_cn, _, _, g_vn, _ = decode_backward(g, cfg, x, T, gy, list(outs), saved, w_cn=wc, w_vn=wv)
+        res[tied] = (outs, g_cn.double().sum(1), g_vn)
+    assert torch.equal(res[False][0], res[True][0])
+    a, b = res[False][1].cpu().numpy(), res[True][1].cpu().numpy()
+    np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-6 * np.abs(a).max())
+    assert torch.equal(res[False][2], res[True][2])
+
+
 @pytest.mark.parametrize("q", [0, 2])
 def test_qms_inactive_quantiser_runs_on_streaming_path(q):
     """QMS with a qbit the reference's quantiser does not know (Boosted…py:187-214: the message passes
