@@ -165,6 +165,7 @@ EARLYVN = os.environ.get("NLDPC_GEN_EARLYVN", "0") == "1"
 # per part like the untied kernel (0, default): cfg5 backward 28.33 vs 27.87 ms, step 46.09 vs 45.65 ms
 # (same box, profiles/r4c_ab_cfg5.txt) -- the units form spilled more (139 VGPRs against 66)
 TIED_UNITS = os.environ.get("NLDPC_GEN_TIEDUNITS", "0") == "1"
+BWDSB = int(os.environ.get("NLDPC_GEN_BWDSB", "2"))  # backward check rows: 1 = fence per row, 2 = per copy
 NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"
 
 # experiment knob: check-node writes (c2v back into the chunk image) by ds_write_addtid_b32 -- address = M0 +
@@ -1586,7 +1587,11 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     w("template <int KIND, int DC, int TIED, int Q0, int Q1>  // the row's copies Q0 .. Q1-1")
     w("__device__ __forceinline__ void cnb_row(float* rp, const char* sq, int u, const FusedBwdArgs& a, int it, "
       "int e0, int row, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
-    w("    __builtin_amdgcn_sched_barrier(0);  // one row at a time (register pressure)")
+    # NLDPC_GEN_BWDSB bit 0: a scheduling fence before each row; bit 1: after each lane copy.  Default 2
+    # (per copy only): the row fence pushed the tied QMS kernel to 123 VGPR spills (21 without) and cfg5's
+    # backward measured 27.97 -> 27.32 ms without it (0 = no fence at all: 27.49; profiles/r4_ab.txt)
+    if BWDSB & 1:
+        w("    __builtin_amdgcn_sched_barrier(0);  // one row at a time (register pressure)")
     w("    float wv[DC], bv[DC];")
     w("    const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + e0) : nullptr;")
     w("    const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + e0) : nullptr;")
@@ -1688,7 +1693,8 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         tied("        ", f"q == {Q - 1}")
         flush_q("            ")
         w("        }")
-    w("        __builtin_amdgcn_sched_barrier(0);  // one check copy at a time: the state owns the registers")
+    if BWDSB & 2:
+        w("        __builtin_amdgcn_sched_barrier(0);  // one check copy at a time: the state owns the registers")
     w("    }")
     if not GWQ:
         tied("    ", "true")
