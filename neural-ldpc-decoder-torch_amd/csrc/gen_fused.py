@@ -165,6 +165,9 @@ EARLYVN = os.environ.get("NLDPC_GEN_EARLYVN", "0") == "1"
 # per part like the untied kernel (0, default): cfg5 backward 28.33 vs 27.87 ms, step 46.09 vs 45.65 ms
 # (same box, profiles/r4c_ab_cfg5.txt) -- the units form spilled more (139 VGPRs against 66)
 TIED_UNITS = os.environ.get("NLDPC_GEN_TIEDUNITS", "0") == "1"
+# experiment: the check-node weights loaded at the start of their check-node phase instead of a phase
+# ahead (one chunk's weights live in SGPRs at a time instead of two)
+WLATE = os.environ.get("NLDPC_GEN_WLATE") == "1"
 BWDSB = int(os.environ.get("NLDPC_GEN_BWDSB", "2"))  # backward check rows: 1 = fence per row, 2 = per copy
 NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"
 
@@ -1323,10 +1326,13 @@ def emit(S: Spec) -> str:
             return f"lds + {(ci % S.nbuf) * CF}" if S.nbuf > 1 else "lds"
 
         def op_w(ci):
-            preload(ci)
+            if not WLATE:
+                preload(ci)
             w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, it, sv, vc);")
 
         def op_cn(ci):
+            if WLATE:
+                preload(ci)
             if "cn" not in SKIP:
                 w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw, xr, apr, cdm);")
 
