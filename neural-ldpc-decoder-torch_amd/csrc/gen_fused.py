@@ -165,9 +165,12 @@ EARLYVN = os.environ.get("NLDPC_GEN_EARLYVN", "0") == "1"
 # per part like the untied kernel (0, default): cfg5 backward 28.33 vs 27.87 ms, step 46.09 vs 45.65 ms
 # (same box, profiles/r4c_ab_cfg5.txt) -- the units form spilled more (139 VGPRs against 66)
 TIED_UNITS = os.environ.get("NLDPC_GEN_TIEDUNITS", "0") == "1"
-# experiment: the check-node weights loaded at the start of their check-node phase instead of a phase
-# ahead (one chunk's weights live in SGPRs at a time instead of two)
-WLATE = os.environ.get("NLDPC_GEN_WLATE") == "1"
+# When a chunk's check-node weights are loaded: a phase ahead (with the chunk's owner writes; Neural) or at
+# the start of its check-node phase (one chunk's weights in SGPRs at a time instead of two; Boosted, whose
+# kernels spilled SGPRs: cfg3ucn MS NW(1,1,2) 97.3 -> 92.6 ms, QMS 100.1 -> 99.8, profiles/r4_ab.txt).
+# NLDPC_GEN_WLATE: "boosted" (default), "0" every kind early, "1" every kind late
+WLATE = os.environ.get("NLDPC_GEN_WLATE", "boosted")
+WLATE_COND = {"boosted": "KIND != NLDPC_NEURAL", "0": "false", "1": "true"}[WLATE]
 BWDSB = int(os.environ.get("NLDPC_GEN_BWDSB", "2"))  # backward check rows: 1 = fence per row, 2 = per copy
 NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"
 
@@ -1298,11 +1301,15 @@ def emit(S: Spec) -> str:
         w("        (void)sv; (void)svb;")
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
         stamp(1)
+        def declare_w(ci):
+            nw = S.cn_nw[(p, ci)]
+            w(f"        float W{ci}[{nw}], B{ci}[{nw}];")
+
         def preload(ci):
             nw = S.cn_nw[(p, ci)]
             # this chunk's check-node weights, by whole-row scalar loads issued a phase ahead of its check
-            # nodes (their latency overlaps LDS traffic and a barrier, not the check rows' LDS waits)
-            w(f"        float W{ci}[{nw}], B{ci}[{nw}];")
+            # nodes (their latency overlaps LDS traffic and a barrier, not the check rows' LDS waits), or
+            # at the start of the check-node phase (WLATE)
             w("        {")
             w("            const cfloat_p wc_ = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E) : nullptr;")
             w("            const float* bsrc_ = KIND == NLDPC_NEURAL ? a.bias : (a.ucn ? a.w_ucn : nullptr);  // bias / UCN weight")
@@ -1326,13 +1333,14 @@ def emit(S: Spec) -> str:
             return f"lds + {(ci % S.nbuf) * CF}" if S.nbuf > 1 else "lds"
 
         def op_w(ci):
-            if not WLATE:
-                preload(ci)
+            declare_w(ci)
+            w(f"        if constexpr (!({WLATE_COND}))")
+            preload(ci)
             w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, it, sv, vc);")
 
         def op_cn(ci):
-            if WLATE:
-                preload(ci)
+            w(f"        if constexpr ({WLATE_COND})")
+            preload(ci)
             if "cn" not in SKIP:
                 w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw, xr, apr, cdm);")
 
