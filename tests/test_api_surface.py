@@ -110,6 +110,33 @@ def test_boosted_fetch_param_temporal_and_constraints():
     assert len(m.get_trainable_parameters()) == 8  # iterations < 2 are frozen
 
 
+def test_boosted_tied_rows_and_multi_tensor_clamps():
+    """Sharing code 3: the rows the forward stacks as one expand of the stacked scalars (_tied_rows) equal
+    the per-iteration expands (_iteration_weights), and their gradient reaches every parameter; the
+    multi-tensor _apply_constraints equals clamp_(lo, hi) per parameter, values outside on both sides."""
+    from boosted_neural_ldpc_decoder.struct.NodeType import NodeType
+    m = _boosted((3, 3, 3), T=5)
+    g = torch.Generator().manual_seed(3)
+    with torch.no_grad():
+        for p_ in m.parameters():
+            p_.copy_(torch.randn(p_.shape, generator=g) * 3)
+    run = [0, 1, 2, 3, 4]
+    for nt, width in ((NodeType.CN, int(m.sum_edge)), (NodeType.UCN, int(m.sum_edge)), (NodeType.VN, m.N)):
+        rows = m._tied_rows(nt, run, width)
+        k = {NodeType.CN: 0, NodeType.UCN: 1, NodeType.VN: 2}[nt]
+        ref = torch.stack([m._iteration_weights(t, [], None, 0, torch.device("cpu"))[k] for t in run])
+        assert torch.equal(rows, ref)
+    rows = m._tied_rows(NodeType.CN, run, int(m.sum_edge))
+    rows.sum().backward()
+    for t in run:
+        assert float(m.weight_CN_3.grad if t == 3 else getattr(m, f"weight_CN_{t}").grad) == float(m.sum_edge)
+    want = {n: p_.detach().clone().clamp_(m.allowed_weight_range.start, m.allowed_weight_range.end)
+            for n, p_ in m.named_parameters()}
+    m._apply_constraints()
+    for n, p_ in m.named_parameters():
+        assert torch.equal(p_.detach(), want[n]), n
+
+
 def test_neural_parameters_and_state_dict_compat():
     import neural_ldpc_decoder as nd
     conn = nd.ConnectingMatrixTorch(nd.ConnectingMatrix(16, BG2))
