@@ -165,6 +165,9 @@ EARLYVN = os.environ.get("NLDPC_GEN_EARLYVN", "0") == "1"
 # per part like the untied kernel (0, default): cfg5 backward 28.33 vs 27.87 ms, step 46.09 vs 45.65 ms
 # (same box, profiles/r4c_ab_cfg5.txt) -- the units form spilled more (139 VGPRs against 66)
 TIED_UNITS = os.environ.get("NLDPC_GEN_TIEDUNITS", "0") == "1"
+# UCN flag of a check copy (per-copy form): the row's hard-decision words all read from LDS before the
+# shifts and XORs (1), instead of one read-shift-XOR per edge (0: hipcc waited on each read in turn)
+UCNB = os.environ.get("NLDPC_GEN_UCNB", "1") == "1"
 # When a chunk's check-node weights are loaded: a phase ahead (with the chunk's owner writes; Neural) or at
 # the start of its check-node phase (one chunk's weights in SGPRs at a time instead of two; Boosted, whose
 # kernels spilled SGPRs: cfg3ucn MS NW(1,1,2) 97.3 -> 92.6 ms, QMS 100.1 -> 99.8, profiles/r4_ab.txt).
@@ -984,11 +987,23 @@ def emit(S: Spec) -> str:
                     w(f"            if constexpr (UCNW) uf_ = __builtin_amdgcn_inverse_ballot_w64(umr{i}_{q}) ? 1.f : 0.f;")
                     w("            else {")
                 w("            uint32_t par_ = 0;")
+                if UCNB:  # every word of the row requested first, then the shifts and XORs (one LDS wait, not DC)
+                    ks = [(k, e) for k, e in enumerate(es) if e not in d1set]
+                    for k, e in ks:
+                        c, dvu = rot(e, q)
+                        j = int(S.hb_cols[e])
+                        # (u + c) mod Z as min(v, v - Z) on unsigned: v - Z wraps above v unless v >= Z
+                        vexpr = f"(uint32_t)u + {c}u" if c + ZT <= Z else f"min((uint32_t)u + {c}u, (uint32_t)u + {c - Z}u)"
+                        w(f"            const uint32_t v{k}_ = {vexpr}; const uint32_t w{k}_ = appw[{j * S.WZX} + (v{k}_ >> 5)];")
+                    for k, e in ks:
+                        w(f"            par_ ^= w{k}_ >> (v{k}_ & 31u);")
                 for k, e in enumerate(es):
                     c, dvu = rot(e, q)
                     j = int(S.hb_cols[e])
                     vexpr = f"u + {c}" if c + ZT <= Z else f"u + {c} - (u >= {Z - c} ? {Z} : 0)"
                     rd_ = f"{{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZX} + (v_ >> 5)] >> (v_ & 31); }}"
+                    if UCNB and e not in d1set:
+                        continue
                     if e in d1set:  # bypass: the hard decision of this thread's own previous posterior
                         ix = S.cd_index[p].index((e, q))
                         app0 = f"(a.first_iter > 0 ? bload(apr, vo + {dvu}, {4 * (j * Z + c)}) : chan<KIND>(cd[{ix}], a))"
