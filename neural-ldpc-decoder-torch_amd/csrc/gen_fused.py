@@ -173,6 +173,9 @@ UCNB = os.environ.get("NLDPC_GEN_UCNB", "1") == "1"
 # kernels spilled SGPRs: cfg3ucn MS NW(1,1,2) 97.3 -> 92.6 ms, QMS 100.1 -> 99.8, profiles/r4_ab.txt).
 # NLDPC_GEN_WLATE: "boosted" (default), "0" every kind early, "1" every kind late
 WLATE = os.environ.get("NLDPC_GEN_WLATE", "boosted")
+# with WLATE: a pipelined phase's check-node weights are requested at the start of the phase, before the
+# owner writes / read-backs it also runs (their latency hidden behind that work; still one chunk in SGPRs)
+WPHASE = os.environ.get("NLDPC_GEN_WPHASE", "0") == "1"
 WLATE_COND = {"boosted": "KIND != NLDPC_NEURAL", "0": "false", "1": "true"}[WLATE]
 BWDSB = int(os.environ.get("NLDPC_GEN_BWDSB", "2"))  # backward check rows: 1 = fence per row, 2 = per copy
 NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"
@@ -1353,9 +1356,10 @@ def emit(S: Spec) -> str:
             preload(ci)
             w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, it, sv, vc);")
 
-        def op_cn(ci):
-            w(f"        if constexpr ({WLATE_COND})")
-            preload(ci)
+        def op_cn(ci, loaded=False):
+            if not loaded:
+                w(f"        if constexpr ({WLATE_COND})")
+                preload(ci)
             if "cn" not in SKIP:
                 w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw, xr, apr, cdm);")
 
@@ -1392,8 +1396,17 @@ def emit(S: Spec) -> str:
                     setprio(p, k)
                 elif k > 0:
                     setprio(p, 0)  # [R_{K-1}] belongs to the next VN phase
+                early_w = WPHASE and any(kd == "cn" for kd, _ in ph)
+                if early_w:  # WLATE: the phase's check-node weights requested before its other work
+                    for kd, ci in ph:
+                        if kd == "cn":
+                            w(f"        if constexpr ({WLATE_COND})")
+                            preload(ci)
                 for kind_, ci in ph:
-                    {"w": op_w, "cn": op_cn, "r": op_r}[kind_](ci)
+                    if kind_ == "cn":
+                        op_cn(ci, loaded=early_w)
+                    else:
+                        {"w": op_w, "r": op_r}[kind_](ci)
                     if EVN and kind_ == "r" and ci == 1:  # chunks 0-1 are back: the next VN's early sums
                         w(f"        if constexpr (EARLY_VN) {{ if (it + 1 < a.T) vne_p{p}<KIND, MODE>({state_args(p)}{pe_args(p)}); }}")
                 stamp(2 + k)  # arrival at the barrier that ends phase k (stamp 1: after the VN)
