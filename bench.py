@@ -136,6 +136,17 @@ def load_pmc(key):
     return v if isinstance(v, dict) else None
 
 
+def load_isa_budget(kernel):
+    """The committed ISA instruction budget of a kernel (profiles/isa_budget.json, written by
+    tools/isa_budget.py from the gfx950 asm of single-part builds): SIMD issue cycles per workgroup-iteration
+    on the busier SIMD set, the VALU instructions priced at their measured per-class issue costs."""
+    try:
+        v = json.load(open(os.path.join(ROOT, "profiles", "isa_budget.json"))).get(kernel)
+    except (OSError, ValueError):
+        return None
+    return v if isinstance(v, dict) else None
+
+
 def pmc_workload(args):
     """The key of this run's counters in profiles/pmc_traffic.json: the Boosted side lines are keyed by
     decoding type and sharing codes (their kernels differ), e.g. cfg3ucn_QMS_NW112."""
@@ -144,10 +155,13 @@ def pmc_workload(args):
     return args.workload
 
 
-def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings, pmc_key):
+def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings, pmc_key, T=None):
     """Roofline of the dominant kernel: the algorithmic bytes it must move per launch over its average
     HIP-event launch time, against the 8 TB/s HBM spec (and the measured HBM ceilings); HBM traffic
-    and VALU issue from the committed PMC summary of the same workload when present."""
+    and VALU issue from the committed PMC summary of the same workload when present.  `frac` is always
+    the compulsory-byte HBM fraction (the north star's quote); `bound` names the ceiling the evidence says
+    binds: "valu" when the committed ISA budget's issue floor (profiles/isa_budget.json at the PMC effective
+    clock) is a larger fraction of the launch than the bytes are of HBM peak, else "hbm"."""
     per = {}
     for k in KINDS:
         ms_tot, n = prof[k]
@@ -159,7 +173,8 @@ def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings,
     d = per[dom]
     pmc = load_pmc(f"{dom}_{pmc_key}")
     traffic = pmc.get("bytes") if pmc else None
-    r = {"bound": "hbm", "kernel": KERNEL_NAMES[dom].replace("<graph>", graph_tag),
+    kname = KERNEL_NAMES[dom].replace("<graph>", graph_tag)
+    r = {"bound": "hbm", "kernel": kname,
          "achieved": round(d["gbs"], 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
          "frac": round(d["gbs"] / PEAK_HBM_GBS, 4), "traffic": traffic,
          "alg_bytes_per_launch": d["alg_bytes_per_launch"], "avg_launch_ms": round(d["avg_ms"], 4),
@@ -185,6 +200,23 @@ def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings,
                     pmc["valu_insts"] * cyc / (1024 * clk * d["avg_ms"] / 1000.0), 4)
                 r["valu_issue"]["weighted_note"] = ("instructions x mean issue cycles of the kernel's PMC class mix / "
                                                     "(1024 SIMDs x effective clock x launch time): pmc.valu_mix")
+    # the issue floor of the instruction stream (ISA budget), at the clock the PMC pass measured
+    budget = load_isa_budget(pmc.get("kernel") if pmc and pmc.get("kernel") else kname)
+    if budget and T:
+        clk = (pmc.get("effective_clock_ghz") if pmc else None) or budget.get("clock_ghz", 2.4)
+        G = budget.get("G", 1)  # codewords per workgroup of the budgeted geometry
+        wg_iters_per_cu = -(-B // G) / 256.0 * T  # workgroup-iterations per CU (one workgroup per CU at a time)
+        floor_ms = budget["simd_issue_cycles_per_wg_iter"] * wg_iters_per_cu / (clk * 1e9) * 1e3
+        r["issue_floor_ms"] = round(floor_ms, 3)
+        r["issue_frac"] = round(floor_ms / d["avg_ms"], 4)
+        r["issue_floor"] = {"simd_issue_cycles_per_wg_iter": budget["simd_issue_cycles_per_wg_iter"],
+                            "clock_ghz": round(clk, 4), "wg_iters_per_cu": wg_iters_per_cu,
+                            "source": budget.get("source"),
+                            "note": "VALU issue cycles of the busier SIMD set per workgroup-iteration (ISA of the "
+                                    "hot loop at the measured per-class issue costs) x workgroup-iterations per CU / "
+                                    "PMC effective clock: the launch time with no stall at all"}
+        if r["issue_frac"] > r["frac"]:
+            r["bound"] = "valu"
     if dom == "fused" and d5_bytes_per_cw:
         # SURVEY §8(d) D5 models a flooding decoder whose E*Z message state crosses HBM every iteration;
         # the fused kernel keeps that state on chip, so this is an equivalent rate, not traffic
@@ -412,7 +444,8 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
                                                     "frame_errors_last_iter": lit_frames[-1], "frames": B}
     if prof is not None:
         res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T), args.steps, B, Z, world, tag,
-                                   4 * (2 * T * E * Z + (T + 1) * N * Z), ceilings, pmc_workload(args) + f"_B{B}")
+                                   4 * (2 * T * E * Z + (T + 1) * N * Z), ceilings, pmc_workload(args) + f"_B{B}",
+                                   T=T)
     if world == 1 and not args.no_cpu_baseline and not ucn:
         res["cpu_baseline"] = cpu_baseline(bg, Z, T, xa_host, gpu_last, args.cpu_seconds)
     return res

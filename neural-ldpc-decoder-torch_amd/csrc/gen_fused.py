@@ -36,27 +36,44 @@ def app_words(N, Z):
     """32-bit words of one codeword's UCN hard-decision bit array (bit (j, v) = APP[j][v] >= 0): per column
     the Z bits and one more word (word 0 again, so a 32-bit window at any start reads two words)."""
     return N * ((Z + 31) // 32 + 1)
-# check rows up to this degree let the compiler interleave their lane copies (more ILP, more registers)
-CN_PAIR_MAXDC = int(os.environ.get("NLDPC_GEN_CNPAIR", "0"))
-# VN lane copies as packed fp32 pairs (v_pk_add_f32) or all scalar chains.  Measured on gfx950
-# (tools/dev/valu_rate2.hip, profiles/r3_valu_rate2.txt): v_add_f32 issues every 2 cycles per SIMD at
-# >= 2 waves, v_pk_add_f32 every 4 -- the same adds per cycle, so packing buys nothing and costs the
-# register pairs; scalar is the default
-PACK_VN = os.environ.get("NLDPC_GEN_PACK") == "1"
-PACK_MAX = int(os.environ.get("NLDPC_GEN_PACKMAX", "0"))
-# experiment knob: no opaque row base in the check-node phase (lets the compiler prove the row copies'
-# LDS slots disjoint and overlap them, at its own register cost)
-NORO = os.environ.get("NLDPC_GEN_NORO") == "1"
-# Forward chunk schedule.  0: one LDS image of a row chunk at a time, write | check nodes | read-back
-# separated by barriers (every phase is either LDS traffic or VALU work).  1: two LDS buffers of
-# smaller chunks, software-pipelined so that each phase mixes one chunk's check nodes with another
-# chunk's owner writes or read-backs: [VN, W0] [CN0, W1] [R0, CN1] [W2, R1] [CN2, W3] [R2, CN3] ...
-# Default 1 (with CNPIPE: cfg3 kernel 55.2 ms against 58.7 ms for 0/0, tools/gpu_ab.sh, r2)
-PIPE = os.environ.get("NLDPC_GEN_PIPE", "1") == "1"
-# Check-node phase: 1 = software-pipelined row copies (the LDS reads of the next row copy are issued
-# before the current one computes, so the LDS latency hides behind arithmetic instead of stalling)
-CNPIPE = os.environ.get("NLDPC_GEN_CNPIPE", "1") == "1"
-CNDEPTH = int(os.environ.get("NLDPC_GEN_CNDEPTH", "1"))  # row copies whose reads are in flight ahead (experiment)
+# Generator knobs left after the r5 prune (every measured loser is gone; its A/B stays in profiles/):
+#   NLDPC_GEN_PARTS / _SKIP / _STAMPS / _ONLY / _KINDS / _NOBWD   debug and diagnostic builds (above / main)
+#   NLDPC_GEN_GEOM    experiment: override a spec's (G, P, Q)
+#   NLDPC_GEN_WLATE   when a chunk's check-node weights are loaded (below)
+#   NLDPC_FUSED_EXTRA more built-in (graph, Z) pairs
+# Settled choices, no longer knobs (cfg3 kernel ms in the same-box A/B records):
+# * VN lane copies as scalar v_add_f32 chains, two chains (k, k+1) interleaved: packed v_pk_add_f32 pairs issue
+#   at the same adds per cycle on gfx950 (tools/dev/valu_rate2.hip) and spilled (profiles/r2_ab_schedule.txt)
+# * pipelined chunk schedule for the decode / count-only kernels (two LDS buffers, each phase mixes one chunk's
+#   check nodes with another chunk's owner traffic; cfg3 55.2 vs 58.7 ms, r2); the SAVE kernels keep one buffer
+# * check-node row copies software-pipelined one ahead (the next row copy's LDS reads issued before the current
+#   one computes); deeper prefetch 48.5 / 48.8 (profiles/r4_ab.txt)
+# * check-node work balanced by (row, lane copy) units (LPT by degree)
+# * check-row LDS addresses from one 32-bit base per thread (Neural / MS; cfg3 51.7 -> 50.9 ms)
+# * SAVE kernels copy the chunk image to the saved v2c buffer in 16-byte pieces (profiles/r3f_stamps.txt)
+# * backward weight-gradient sums per lane copy (QMS z=384 3135 -> 16 spilled VGPRs), one fence per lane copy
+#   (profiles/r4_ab.txt: 27.97 -> 27.32 ms without the per-row fence)
+# * VN chains keep the reference's explicit "0 +" starts (without them 48.49 -> 48.94 ms, profiles/r3b_ab.txt)
+# * QMS VN as total minus own message (QEXACT, r4: exact on the quantiser's 0.5 grid)
+# * degree-1 bypass for Neural, MS and QMS decode (D1B, r4)
+# * Boosted posterior channel values (cumulative VN weights) requested before a VN call's first store (XPRE=2,
+#   cfg3 MS NW(1,0,2) 99.9 -> 92.5 ms)
+# * UCN flag of a check copy: the row's bit words all read before the shifts and XORs (UCNB, r4p)
+# Removed as measured losers: wave-ballot UCN bits (UCNWAVE, UCNBW), lane-mask wrapped copies (WRAPMASK),
+# paired check rows (CNPAIR, CNPAIR2), owner / check-node ds_write_addtid (OWNTID, CNTID), s_setprio by phase
+# (PRIO), early VN sums in the LDS-only phase (EARLYVN), owner-traffic-aware CN balance (CNBAL_ALPHA), phase
+# weight loads (WPHASE), tied backward by units (TIEDUNITS), QMS wave UCN (UCNW_QMS), no row-base barrier (NORO).
+
+# When a chunk's check-node weights are loaded: a phase ahead (with the chunk's owner writes; Neural) or at
+# the start of its check-node phase (one chunk's weights in SGPRs at a time instead of two; Boosted, whose
+# kernels spilled SGPRs: cfg3ucn MS NW(1,1,2) 97.3 -> 92.6 ms, QMS 100.1 -> 99.8, profiles/r4_ab.txt).
+# NLDPC_GEN_WLATE: "boosted" (default), "0" every kind early, "1" every kind late
+WLATE = os.environ.get("NLDPC_GEN_WLATE", "boosted")
+WLATE_COND = {"boosted": "KIND != NLDPC_NEURAL", "0": "false", "1": "true"}[WLATE]
+NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"  # experiment builds without backward kernels (faster)
+# Decode / count-only chunk schedule (Spec sched): "split" (default, r5) or "pipe2" (r2-r4); experiments:
+# "split<K>" forces K chunks, "split@r1,r2,.." the chunks' first rows
+SCHED = os.environ.get("NLDPC_GEN_SCHED", "split")
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
 # chosen by auto_geometry
@@ -82,116 +99,9 @@ for _item in filter(None, os.environ.get("NLDPC_GEN_GEOM", "").split(";")):
     _t, _g = _item.split(":")
     SPECS = [(t, f, z, *[int(v) for v in _g.split(",")]) if t == _t else (t, f, z, g, p, q) for t, f, z, g, p, q in SPECS]
 
-# Boosted with cumulative VN weights: the posterior re-reads xa (the registers hold xin).  vmcnt counts
-# loads and stores together, in order, so a load issued after a posterior store waits for that store.
-# 2 (default) = every such load of a VN call (and of a read-back's degree-1 columns) issued before its
-# first store: cfg3 MS NW(1,0,2) 99.9 -> 92.5 ms, QMS NW(1,1,2) 234.7 -> 215.6 ms; 1 = at the start of
-# each column (slower: 124 -> 130 ms); 0 = next to each posterior
-XPRE = os.environ.get("NLDPC_GEN_XPRE", "2") == "1"
-XPRE2 = os.environ.get("NLDPC_GEN_XPRE", "2") == "2"
-
-# experiment knob: the lanes of a wrapped copy (own / rot) pick their address by a scalar-computed lane
-# mask (1) instead of a per-lane compare and select (0, default).  On gfx950 v_cmp / v_cndmask issue at
-# half the rate of v_add_f32 (tools/dev/valu_rate2.hip, profiles/r3_valu_rate2*.txt), but the 64-bit
-# masks pushed the kernel's SGPRs (weights of two chunks in flight) into spills: cfg3 49.1 -> 51.3 ms
-# (profiles/r3_ab_cn.txt)
-WRAPMASK = os.environ.get("NLDPC_GEN_WRAPMASK", "0") == "1"
-
-# check-node work balanced over the parts by (row, copy) units (1, default) or by whole rows (0)
-CNUNIT = os.environ.get("NLDPC_GEN_CNUNIT", "1") == "1"
-
-# experiment knob: Neural check rows' copies 0 and 1 computed together, epilogue mul/add as packed f32
-CNPAIR2 = os.environ.get("NLDPC_GEN_CNPAIR2") == "1"
-
-# check-row LDS addresses as 32-bit LDS byte offsets from one per-thread base (lu_ + constant: one
-# v_add_u32 per row copy instead of an add and a shift-add): cfg3 kernel 51.7 -> 50.9 ms (default 1; Neural and MS kernels only: QMS 169 -> 198 ms with it)
-ROADDR = os.environ.get("NLDPC_GEN_ROADDR", "1") == "1"
-
-# SAVE kernels: the v2c messages saved for the backward are copied from the check-ordered LDS image in
-# 16-byte pieces after the write phase (1, default: one extra barrier per chunk) instead of one store
-# per message and lane copy in the write phase (0: byte stores for QMS, issue-bound -- the cfg5 forward's
-# write phases were 81K of 125K cycles per iteration, profiles/r3f_stamps.txt)
-SAVECOPY = os.environ.get("NLDPC_GEN_SAVECOPY", "1") == "1"
-
-# backward check nodes: weight-gradient sums per lane copy q, added over the row's copies by lane 0 in LDS
-# (1, default: no per-lane accumulator lives across the copies -- QMS z=384 with 3 chunks 3135 -> 16
-# spilled VGPRs) or per-lane accumulators over the copies, one wave sum per row (0)
-GWQ = os.environ.get("NLDPC_GEN_GWQ", "1") == "1"
-
-# NLDPC_GEN_ZADD=0: VN chains start from their first message. The reference's sums start from a 0 (sgemm with 0/1 weights), but
-# 0 + x == x for every x except -0 (-> +0), and the sign of a zero is never observed: the check node treats
-# +-0 alike (not positive, |m| = 0 masked), +-0 posteriors compare equal and give the same hard decision.
-# Default 1 = keep the explicit "0 +" adds: without them (0) the cfg3 kernel measured 1 % SLOWER (48.49 -> 48.94/49.03 ms,
-# profiles/r3b_ab.txt; register allocation), though they are ~2 % of the VALU instructions
-ZADD = os.environ.get("NLDPC_GEN_ZADD", "1") == "1"
-
-# the wave UCN in the QMS kernels too (r2 measured it slower there, 180 -> 217 ms, before the QMS kernels lost
-# their generic check node in r3)
-UCNW_QMS = os.environ.get("NLDPC_GEN_UCNW_QMS", "0") == "1"
-
-# experiment knob: CN work units balanced together with the owner LDS traffic of the same barrier interval
-CNBAL_ALPHA = float(os.environ.get("NLDPC_GEN_CNBAL_ALPHA", "0"))
-
-# experiment knob: static wave priority per barrier phase (s_setprio 0-3): within each set of parts that
-# share SIMDs (even / odd parts), the part with the most estimated work in a phase issues first, so the
-# heaviest waves are not left to finish alone at the phase's end (issue is arbitrated by priority, then age)
-PRIO = os.environ.get("NLDPC_GEN_PRIO", "0") == "1"
-
-# QMS variable nodes by total minus own message (1, default): every QMS VN input (the quantised channel
-# value or xin, and the quantised check messages) lies on the quantiser's 0.5 grid with magnitude <= 15.5,
-# so every partial sum of a column (<= 24 terms) is exact in fp32 and any summation order gives the
-# reference's sequential sum bit for bit: v2c_k = (x0 + C) - c_k with C = ((0 + c_0) + c_1) + ... (the
-# posterior's own sum), 2d + 1 adds per column copy instead of d(d-1)/2 + 2d.  (A zero result is +0 in
-# both forms; the check node's conditioning maps either zero to +1e-4 anyway.)
-QEXACT = os.environ.get("NLDPC_GEN_QEXACT", "1") == "1"
-
-# degree-1 bypass for the Boosted MS / QMS decode kernels too (1, default; Neural always has it): the
-# check-node thread holds each degree-1 edge's channel value (xin, advanced by the cumulative VN weights
-# in place), forms its v2c, its posterior and -- UCN -- its hard decision (kept in a register bit mask:
-# the same thread is the only reader of that bit in the next iteration), so those edges skip the LDS
-# round trip and the owner's divergent UCN bit updates
-D1B = os.environ.get("NLDPC_GEN_D1B", "1") == "1"
-
-# the tied-CN-weight backward kernels (MODE 5, default 1); experiment builds: NLDPC_GEN_TIED=0 leaves them out,
-# NLDPC_GEN_NOBWD=1 every backward kernel (decode-only A/B libraries compile in a fraction of the time)
-TIED_BWD = os.environ.get("NLDPC_GEN_TIED", "1") == "1"
-# Neural decode, pipelined schedule with >= 3 chunks: the VN sums over a column's edges in chunks 0-1 run
-# right after those messages are read back (the [W2, R1] phase, which has LDS traffic and no check-node
-# work), the rest in the VN phase.  Exact: the reference's left fold S_k = ((P_{k-1} + c_{k+1}) + ...)
-# splits at any edge; E_k (the fold up to the last early edge) replaces c_k in its register, which no
-# later sum reads, and the prefix P_{m-1} waits in one register per column copy.
-EARLYVN = os.environ.get("NLDPC_GEN_EARLYVN", "0") == "1"
-# the tied kernel's check-node work as (row, lane copy) units balanced over the parts (1) or as whole rows
-# per part like the untied kernel (0, default): cfg5 backward 28.33 vs 27.87 ms, step 46.09 vs 45.65 ms
-# (same box, profiles/r4c_ab_cfg5.txt) -- the units form spilled more (139 VGPRs against 66)
-TIED_UNITS = os.environ.get("NLDPC_GEN_TIEDUNITS", "0") == "1"
-# UCN flag of a check copy (per-copy form): the row's hard-decision words all read from LDS before the
-# shifts and XORs (1), instead of one read-shift-XOR per edge (0: hipcc waited on each read in turn)
-UCNB = os.environ.get("NLDPC_GEN_UCNB", "1") == "1"
-# When a chunk's check-node weights are loaded: a phase ahead (with the chunk's owner writes; Neural) or at
-# the start of its check-node phase (one chunk's weights in SGPRs at a time instead of two; Boosted, whose
-# kernels spilled SGPRs: cfg3ucn MS NW(1,1,2) 97.3 -> 92.6 ms, QMS 100.1 -> 99.8, profiles/r4_ab.txt).
-# NLDPC_GEN_WLATE: "boosted" (default), "0" every kind early, "1" every kind late
-WLATE = os.environ.get("NLDPC_GEN_WLATE", "boosted")
-# with WLATE: a pipelined phase's check-node weights are requested at the start of the phase, before the
-# owner writes / read-backs it also runs (their latency hidden behind that work; still one chunk in SGPRs)
-WPHASE = os.environ.get("NLDPC_GEN_WPHASE", "0") == "1"
-WLATE_COND = {"boosted": "KIND != NLDPC_NEURAL", "0": "false", "1": "true"}[WLATE]
-BWDSB = int(os.environ.get("NLDPC_GEN_BWDSB", "2"))  # backward check rows: 1 = fence per row, 2 = per copy
-NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"
-
-# experiment knob: check-node writes (c2v back into the chunk image) by ds_write_addtid_b32 -- address = M0 +
-# offset + 4 * lane, no address VGPR, twice the LDS store rate of ds_write_b32 on gfx950
-# (tools/dev/addtid_probe.hip) -- on geometries whose waves hold 64 consecutive copies of one codeword
-CNTID = os.environ.get("NLDPC_GEN_CNTID", "0") == "1"
-
-# experiment knob: the owners' v2c writes into the chunk image by ds_write_addtid_b32 as well: no address VALU
-# at all (a copy whose shifted range wraps inside the wave writes twice, each half under its own EXEC mask
-# from the scalar unit), twice the LDS store rate; same geometries as CNTID
-OWNTID = os.environ.get("NLDPC_GEN_OWNTID", "0") in ("1", "2", "3")
-OWNTID_MODE = int(os.environ.get("NLDPC_GEN_OWNTID", "0"))  # (debug) 2: only unwrapped copies, 3: only wrapped
 
 MAX_STATE_REGS = 72  # register-resident c2v floats per thread (the z=384 kernel holds 69 at 124 VGPRs)
+REG_ROOM = 81  # state + degree-1 channel values per thread (r4's z=384 part 0: 69 + 12, no VGPR spills)
 
 
 def auto_geometry(hb, Z):
@@ -250,12 +160,23 @@ def balance(items, weight, P):
 
 
 class Spec:
-    def __init__(self, tag, hb, Z, G, P, Q, pipe=False, stage=0):
-        """stage (backward kernels): bytes per message of the saved v2c staged in LDS beside the chunk
+    def __init__(self, tag, hb, Z, G, P, Q, sched="one", stage=0):
+        """sched: the per-iteration chunk schedule -- "one" (one LDS image: write | check nodes | read-back
+        per chunk; the SAVE kernels), "pipe2" (two buffers, r2) or "split" (two buffers over the compacted
+        image, split barriers, r5: the decode and count-only kernels); see emit().
+        stage (backward kernels): bytes per message of the saved v2c staged in LDS beside the chunk
         image (4 fp32, 1 QMS int8 codes; 0 = none, the check nodes gather from global memory)."""
         assert Z % Q == 0
         self.tag, self.hb, self.Z, self.G, self.P, self.Q = tag, hb, Z, G, P, Q
-        self.pipe = pipe
+        kforce = None
+        if sched.startswith("split@"):  # (a cut list for another graph's rows: the automatic choice)
+            cuts = tuple(int(r) for r in sched[6:].split(","))
+            sched, kforce = "split", (cuts if max(cuts) < hb.shape[0] else None)
+        elif sched.startswith("split") and sched != "split":
+            sched, kforce = "split", int(sched[5:])
+        assert sched in ("one", "pipe2", "split"), sched
+        self.sched = sched
+        self.pipe = sched != "one"  # two LDS buffers (not the SAVE kernels' schedule)
         self.ZT = Z // Q
         self.M, self.N = hb.shape
         rows, cols = np.nonzero(hb != -1)
@@ -270,7 +191,7 @@ class Spec:
         # waves of a workgroup go round the 4 SIMDs, so with 2-wave parts the even parts share SIMDs
         # {0,1} and the odd parts SIMDs {2,3}; the VN phase saturates the SIMDs, so order the parts
         # for equal VN work (sequential adds per lane copy) on the two sets
-        if P == 8 and G * self.ZT == 128 and os.environ.get("NLDPC_GEN_SIMDBAL", "1") == "1":
+        if P == 8 and G * self.ZT == 128:
             import itertools
             cost = [sum(deg(j) * (deg(j) - 1) // 2 + 2 * deg(j) + 1 for j in c) for c in self.reg_cols]
             best = min(itertools.combinations(range(P), P // 2),
@@ -283,20 +204,6 @@ class Spec:
         # row chunks: contiguous row ranges whose messages (edges x Z x G) fit in LDS beside the UCN bits
         self.WZ = (Z + 31) // 32
         self.WZX = self.WZ + 1  # words per column in the bit array
-        # UCN by waves: every wave's 64 lanes are 64 consecutive copies of one codeword (ZT % 64 == 0) and
-        # the bit vectors are whole words (Z % 32 == 0).  The owners write the hard decisions by ballots
-        # (no LDS atomics, no clearing), and a check row's unsatisfied flags come from word windows of
-        # its columns' vectors XOR-ed once per row and wave, not gathered bit by bit per copy and edge.
-        # (used by the MS kernels only: in the QMS kernels the extra scalar state measured slower, 180 -> 217 ms
-        # at cfg3 NW(1,1,2), register allocation; UCNW in the generated code)
-        # r3: off by default -- after the r3 kernel changes the per-copy form is faster for MS too (cfg3 MS
-        # NW(1,1,2) + UCN kernel 111.6 -> 107.6 ms, same-box A/B, profiles/r3t_ab_ms_ucnw.txt)
-        self.ucn_wave = self.ZT % 64 == 0 and Z % 32 == 0 and os.environ.get("NLDPC_GEN_UCNWAVE", "0") == "1"
-        # UCN hard decisions written by wave ballots (no LDS atomics, no clearing pass and barrier), the check
-        # side still gathering one bit per copy and edge: any geometry whose waves hold 64 consecutive copies
-        # of one codeword (the owner half of ucn_wave without its window-XOR check side)
-        self.ucn_bw = (not self.ucn_wave and self.ZT % 64 == 0 and Z % 32 == 0
-                       and os.environ.get("NLDPC_GEN_UCNBW", "0") == "1")
         self.lanes = G * self.ZT  # live threads per part
         # A part occupies whole waves.  The lanes past the live ones (padded parts) run the code of the
         # first live lanes (same copies) on an LDS region of their own and with global offsets out of
@@ -311,8 +218,18 @@ class Spec:
         GL = self.G_lds
         cap = ((LDS_BYTES - 4 * GL * app_words(self.N, Z)) // (4 * GL) - 32) // Z
         row_max = max(len(r) for r in self.row_edges)
-        if pipe:  # two buffers; only the count-only counters (G*128 B) share the remaining KiB
+        if self.pipe:  # two buffers; only the count-only counters (G*128 B) share the remaining KiB
             cap = ((160 * 1024 - 1024 - 4 * GL * app_words(self.N, Z)) // (8 * GL) - (32 if GL > 1 else 0)) // Z
+        # LDS slot of each edge in a chunk image.  "split": the image is compacted to the edges of the
+        # columns of degree > 1 -- every decode kind bypasses LDS for its degree-1 edges (D1_BYPASS), so the
+        # 38 degree-1 slots of BG2 would never be written -- and a chunk's slots are consecutive (C order).
+        d1e = {self.col_edges[j][0] for j in single}
+        self.compact = sched == "split"
+        self.slot = {}
+        for e in range(self.E):
+            if not (self.compact and e in d1e):
+                self.slot[e] = len(self.slot)
+        self.NS = len(self.slot)
 
         def chunking(cap, stage):
             chunks, r0 = [], 0  # (row_begin, row_end, edge_begin, edge_end)
@@ -332,7 +249,10 @@ class Spec:
             sf = -(-(max(e1 - e0 for _, _, e0, e1 in chunks) * Z * stage) // 16) * 4 if stage else 0
             return chunks, cf, sf
 
-        if stage:  # the largest chunks whose image and staged messages fit beside each other
+        if sched == "split":
+            self._split_chunks(d1e, kforce)
+            got = (self.chunks, None, 0)
+        elif stage:  # the largest chunks whose image and staged messages fit beside each other
             c = cap
             while c >= row_max:
                 got = chunking(c, stage)
@@ -343,10 +263,15 @@ class Spec:
                 stage = 0  # a row and its staged messages do not fit: gather from global memory
             if stage:
                 cap = c
-        got = chunking(cap, stage)
-        if got is None:
-            raise SystemExit(f"{tag}: a single check row does not fit in LDS")
-        self.chunks, self.chunk_floats, self.stage_floats = got
+        if sched != "split":
+            got = chunking(cap, stage)
+            if got is None:
+                raise SystemExit(f"{tag}: a single check row does not fit in LDS")
+            self.chunks, self.chunk_floats, self.stage_floats = got
+            self.nbuf = 2 if self.pipe and len(self.chunks) > 1 else 1  # (one chunk: the second buffer would stay unused)
+            # LDS float offset of chunk c's image in a codeword's block, and the block's size
+            self.region_off = [(c % self.nbuf) * self.chunk_floats for c in range(len(self.chunks))]
+            self.cw_floats = self.chunk_floats * self.nbuf
         self.stage = stage
         # LDS-DMA width of the staging: 16 B when every chunk's block (and the per-codeword stride of
         # the saved buffer) is a multiple of 16 B, else 4 B
@@ -355,42 +280,79 @@ class Spec:
             4 if stage and all(o % 4 == 0 and n % 4 == 0 for o, n in blocks) else 0
         if stage and not self.stage_width:
             self.stage, self.stage_floats = 0, 0
-        self.nbuf = 2 if pipe and len(self.chunks) > 1 else 1  # (one chunk: the second buffer would stay unused)
         self.cn_rows = [balance(list(range(r0, r1)), lambda i: len(self.row_edges[i]), P)
                         for (r0, r1, _, _) in self.chunks]
         # forward check-node work units (row i, lane copy q) of each chunk, balanced over the parts by
         # degree (LPT): a row's Q copies may go to different parts.  A check-node phase is bound by
         # its busiest wave (a chain of LDS round trips, one per row copy), and whole rows balanced
         # badly: BG2 z=384 chunk 0 has 7 rows for 8 parts (edge copies per lane 30, 30, 24, 24, 18,
-        # 18, 12, 0; by units at most 21).  NLDPC_GEN_CNUNIT=0: whole rows (cn_rows)
-        if CNUNIT:
-            self.cn_units = []
-            K = len(self.chunks)
-
-            def owner_msgs(p, c):  # register messages part p writes / reads back for chunk c
-                if c < 0 or c >= K:
-                    return 0
-                e0, e1 = self.chunks[c][2], self.chunks[c][3]
-                return Q * sum(1 for e in self.slots[p] if e0 <= e < e1)
-            for ci, (r0, r1, _, _) in enumerate(self.chunks):
-                units = sorted(((i, q) for i in range(r0, r1) for q in range(Q)),
-                               key=lambda iq: (-len(self.row_edges[iq[0]]), iq[0], iq[1]))
-                # CNBAL_ALPHA > 0 (pipelined schedule): start each part's load at the owner LDS traffic it
-                # runs in the same barrier interval (CN_c with W_{c+1} for even c, with R_{c-1} for odd c),
-                # priced at alpha check-node edge copies per message
-                partner = (ci + 1) if ci % 2 == 0 else (ci - 1)
-                load = [CNBAL_ALPHA * owner_msgs(p_, partner) if pipe else 0 for p_ in range(P)]
-                bins = [[] for _ in range(P)]
-                for i, q in units:
-                    k = int(np.argmin(load))
-                    bins[k].append((i, q))
-                    load[k] += len(self.row_edges[i]) + 1  # + the row's fixed work
-                self.cn_units.append([sorted(b, key=lambda iq: (-len(self.row_edges[iq[0]]), iq[0], iq[1])) for b in bins])
-        else:
-            self.cn_units = [[[(i, q) for i in sorted(rows, key=lambda i: -len(self.row_edges[i])) for q in range(Q)]
-                              for rows in self.cn_rows[ci]] for ci in range(len(self.chunks))]
+        # 18, 12, 0; by units at most 21)
+        # Register room: a unit's degree-1 edges stay in its part's registers for the whole decode (D1_BYPASS,
+        # `cd`), on top of the part's state; a part is offered a unit only while state + cd fits REG_ROOM (the
+        # z=384 parts 0/1 hold 69/66 state floats), else the least-loaded part takes it anyway.
+        nd1 = [sum(1 for e in self.row_edges[i] if e in d1e) for i in range(self.M)]
+        regs = [Q * len(sl) for sl in self.slots]
+        self.cn_units = []
+        for ci, (r0, r1, _, _) in enumerate(self.chunks):
+            units = sorted(((i, q) for i in range(r0, r1) for q in range(Q)),
+                           key=lambda iq: (-len(self.row_edges[iq[0]]), iq[0], iq[1]))
+            load = [0] * P
+            bins = [[] for _ in range(P)]
+            for i, q in units:
+                fit = [k for k in range(P) if regs[k] + nd1[i] <= REG_ROOM]
+                k = min(fit or range(P), key=lambda k_: (load[k_], k_))
+                bins[k].append((i, q))
+                load[k] += len(self.row_edges[i]) + 1  # + the row's fixed work
+                regs[k] += nd1[i]
+            self.cn_units.append([sorted(b, key=lambda iq: (-len(self.row_edges[iq[0]]), iq[0], iq[1])) for b in bins])
         self.max_dc = max(len(r) for r in self.row_edges)
         self.hb_cols = cols  # column of each C-order edge
+
+    def _split_chunks(self, d1e, kforce):
+        """The "split" schedule's chunks: K contiguous row ranges over the compacted image, chunk c in region c % 2
+        (region A for even chunks, B for odd ones: A + B slots fit LDS beside the UCN bits and counters).  An
+        iteration has K + 1 barriers (emit()), so the fewest chunks that fit win; among those, the split whose
+        busiest check-node phase (check rows of chunk k-1 plus the owner traffic of chunks k and k-2) is lightest."""
+        Z, Q, GL = self.Z, self.Q, self.G_lds
+        cap = ((160 * 1024 - 1024 - 4 * GL * app_words(self.N, Z)) // (4 * GL) - (32 if GL > 1 else 0)) // Z
+        nsl = [sum(1 for e in self.row_edges[i] if e not in d1e) for i in range(self.M)]  # LDS slots per row
+        cnw = [len(self.row_edges[i]) + 1 for i in range(self.M)]  # check-node work per row copy
+        pre_s, pre_w = np.concatenate([[0], np.cumsum(nsl)]), np.concatenate([[0], np.cumsum(cnw)])
+        if max(nsl) > cap:
+            raise SystemExit(f"{self.tag}: a single check row does not fit in LDS")
+        import itertools
+        best = None
+        for K in ([len(kforce) + 1] if isinstance(kforce, tuple) else [kforce] if kforce else range(1, self.M + 1)):
+            for cut in ([kforce] if isinstance(kforce, tuple) else itertools.combinations(range(1, self.M), K - 1)):
+                b = (0,) + cut + (self.M,)
+                sl = [int(pre_s[b[c + 1]] - pre_s[b[c]]) for c in range(K)]
+                A = max(sl[0::2])
+                B = max(sl[1::2]) if K > 1 else 0
+                if A + B > cap or min(sl) == 0 and K > 1:
+                    continue
+                cn = [int(pre_w[b[c + 1]] - pre_w[b[c]]) for c in range(K)]
+                own = lambda c: sl[c] if 0 <= c < K else 0  # noqa: E731
+                load = [cn[k - 1] + 0.25 * (own(k) + own(k - 2)) for k in range(1, K + 1)]
+                key = (max(load), sum(x * x for x in load))
+                if best is None or key < best[0]:
+                    best = (key, b, A, B)
+            if best is not None:
+                break
+        if best is None:
+            raise SystemExit(f"{self.tag}: no split chunking fits LDS")
+        _, b, A, B = best
+        self.chunks = []
+        for c in range(len(b) - 1):
+            s0 = int(pre_s[b[c]])
+            self.chunks.append((b[c], b[c + 1], s0, int(pre_s[b[c + 1]])))
+        self.region_slots = (A, B)
+        self.region_off = [0 if c % 2 == 0 else A * Z for c in range(len(self.chunks))]
+        cw = (A + B) * Z
+        if GL > 1:  # codeword stride = 1 (mod 32 banks) so lanes of different codewords do not collide
+            cw += (1 - cw) % 32
+        self.cw_floats = cw
+        self.chunk_floats = max(A, B) * Z
+        self.nbuf = 2 if len(self.chunks) > 1 else 1
 
 
 def emit(S: Spec) -> str:
@@ -399,10 +361,11 @@ def emit(S: Spec) -> str:
     w = L.append
     CF = S.chunk_floats
     # wrapped lane copies by scalar lane masks (own_lv): needs waves of 64 consecutive copies of one codeword
-    WRAPM = WRAPMASK and G == 1 and ZT % 64 == 0
     w(f"// ---- {S.tag}: M={S.M} N={S.N} E={S.E} Z={Z}; workgroup = {G} codeword(s) x {S.P} part(s) x {ZT} lanes "
       f"= {S.threads} threads{' (padded parts)' if S.padded else ''}, {Q} cop{'y' if Q == 1 else 'ies'} per lane; register slots/part "
-      f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B")
+      f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B; schedule {S.sched}"
+      + (f", regions {S.region_slots} slots, chunks {[(c[0], c[1], c[3] - c[2]) for c in S.chunks]} (rows, slots)"
+         if S.sched == "split" else ""))
     w(f"namespace fused_{S.tag} {{")
     w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E};")
     w("// degree-1 edges bypass LDS (Neural inference; see the check-node section)")
@@ -412,203 +375,124 @@ def emit(S: Spec) -> str:
     w("#define SAVE (MODE == 1)")
     w("#define CNT (MODE >= 2)")
     w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
-    d1b = D1B and not S.ucn_wave  # (the window-XOR UCN check side reads the degree-1 columns' LDS words)
-    w(f"#define D1_BYPASS ((KIND == NLDPC_NEURAL{' || KIND == NLDPC_MS || KIND == NLDPC_QMS' if d1b else ''}) && !SAVE)")
-    w(f"#define EARLY_VN ({'KIND == NLDPC_NEURAL && !SAVE' if EARLYVN and S.pipe and len(S.chunks) >= 3 else 'false'})"
-      "  // VN sums split around the [W2, R1] phase (EARLYVN)")
+    w("#define D1_BYPASS (!SAVE)")
     w("// check-row LDS addresses from one 32-bit base (ROADDR); in the QMS / SP kernels it measured slower")
     w("#define ROA (KIND == NLDPC_NEURAL || KIND == NLDPC_MS)")
-    w(f"#define UCNW ((KIND == NLDPC_MS{' || KIND == NLDPC_QMS' if UCNW_QMS else ''}) && {'true' if S.ucn_wave else 'false'})  "
-      "// UCN bits by waves (Spec.ucn_wave)")
     assert NZ < 65536  # per-codeword error counts are packed two to an LDS word
 
-    # Register state of part p: copies are paired (q = 0,1 / 2,3 ...) into float2 arrays so the VN's
-    # additions run as packed fp32 (v_pk_add_f32: two IEEE adds per lane, same rounding); an odd
-    # copy count leaves one scalar array.  The channel values a thread needs every iteration are
-    # loaded once into registers (xp*/xs for its register columns, xd for its degree-1 columns).
-    # per part: PACK_VN packs every part; PACK_MAX packs the parts whose register state (slots x Q)
-    # stays within that many registers (the heavy parts stay scalar, clear of the 128-VGPR cap)
-    def NP(p):
-        return Q // 2 if (PACK_VN or len(S.slots[p]) * Q <= PACK_MAX) else 0
-
-    def NS(p):
-        return Q - 2 * NP(p)
-
-    # EARLYVN (see the knob): the early VN sums cover each column's edges below the end of chunk 1
-    EVN = EARLYVN and S.pipe and len(S.chunks) >= 3 and all(NP(p_) == 0 for p_ in range(S.P))
-    esplit = S.chunks[1][3] if EVN else 0
-
-    def early_m(j):  # the column's edges in chunks 0-1 (its edges are in row order)
-        return sum(1 for e in S.col_edges[j] if e < esplit) if EVN else 0
-
-    def pe_params(p):  # the prefix P_{m-1} of each register column and lane copy, between the two parts
-        return "".join(f", float (&pe{i})[{max(len(S.reg_cols[p]), 1)}]" for i in range(NS(p))) if EVN else ""
-
-    def pe_args(p):
-        return "".join(f", pe{i}" for i in range(NS(p))) if EVN else ""
-
+    # Register state of part p: one float array per lane copy q (cs{q}[slot]).  The channel values a thread
+    # needs every iteration are loaded once into registers (xs{q} for its register columns, xd for its
+    # degree-1 columns).
     def ref(p, q, k):
-        if q < 2 * NP(p):
-            return f"cp{q // 2}[{k}].{'x' if q % 2 == 0 else 'y'}"
-        return f"cs{q - 2 * NP(p)}[{k}]"
+        return f"cs{q}[{k}]"
 
     def xref(p, j, q):
         cols = S.reg_cols[p]
         if j in cols:
-            n = cols.index(j)
-            return f"xp{q // 2}[{n}].{'x' if q % 2 == 0 else 'y'}" if q < 2 * NP(p) else f"xs{q - 2 * NP(p)}[{n}]"
+            return f"xs{q}[{cols.index(j)}]"
         n = S.d1_cols[p].index(j)
         return f"xd[{n * Q + q}]"
 
     def state_params(p, const=False):
         sp = len(S.slots[p])
         c = "const " if const else ""
-        ps = [f"{c}f2 (&cp{i})[{max(sp, 1)}]" for i in range(NP(p))]
-        for i in range(NS(p)):
-            ps.append(f"{c}float (&cs{i})[{max(sp, 1)}]")
-        return ", ".join(ps)
+        return ", ".join(f"{c}float (&cs{i})[{max(sp, 1)}]" for i in range(Q))
 
     def state_args(p):
-        return ", ".join([f"cp{i}" for i in range(NP(p))] + [f"cs{i}" for i in range(NS(p))])
+        return ", ".join(f"cs{i}" for i in range(Q))
 
     def x_params(p):
         nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
-        ps = [f"const f2 (&xp{i})[{nr}]" for i in range(NP(p))]
-        for i in range(NS(p)):
-            ps.append(f"const float (&xs{i})[{nr}]")
+        ps = [f"const float (&xs{i})[{nr}]" for i in range(Q)]
         ps.append(f"const float (&xd)[{nd}]")
         return ", ".join(ps)
 
     def x_args(p):
-        return ", ".join([f"xp{i}" for i in range(NP(p))] + [f"xs{i}" for i in range(NS(p))] + ["xd"])
+        return ", ".join([f"xs{i}" for i in range(Q)] + ["xd"])
+
+    # UCN hard decisions a thread keeps in registers: d1m (its degree-1 columns' posteriors, the non-bypass
+    # kernels) and cdm (bypass: the posteriors of its cd entries) -- bit arrays of 32-bit words, as many as the
+    # part needs (a run-time geometry with few parts can hold more than 32)
+    def nwords(p, which):
+        n = len(S.d1_cols[p]) * Q if which == "d1m" else len(S.cd_index[p])
+        return max(1, -(-n // 32))
+
+    def bit_get(arr, b):
+        return f"({arr}[{b >> 5}] >> {b & 31})"
+
+    def bit_set(arr, b, cond):
+        return f"{arr}[{b >> 5}] = ({arr}[{b >> 5}] & ~(1u << {b & 31})) | (({cond}) ? 1u : 0u) << {b & 31}"
 
     # ---------------------------------------------------------------- variable nodes
     # global accesses: bload/bstore(descriptor, lane byte offset vo, constant byte offset)
     def X(j, q):  # byte offset of variable copy (column j, lane copy q) in a [N][Z] codeword
         return 4 * (j * Z + q * ZT)
 
-    def vn_col(p, n, j, s, d, final, early=False):
-        """VN (or final posterior) of column j (n-th register column of part p) for every copy group of
-        the lane at once: the packed-pair chains (v_pk_add_f32, copies 2i/2i+1) and the scalar chain
-        (last copy) are emitted interleaved, so consecutive adds never depend on each other (gfx950
-        puts an s_nop between two dependent packed adds).  Each chain is the reference's sequential
-        fp32 order: S_k = ((P_{k-1} + c_{k+1}) + ...) + c_{d-1}, v2c_k = x0 + S_k, P_k = P_{k-1} + c_k."""
-        grp = [("f2", f"cp{i}", f"xp{i}[{n}]", str(i)) for i in range(NP(p))]
-        for i in range(NS(p)):
-            grp.append(("float", f"cs{i}", f"xs{i}[{n}]", f"s{i}"))
-
-        def add(T_, x, y):
-            return f"({x} + {y})" if T_ == "f2" else f"fadd({x}, {y})"
-
-        def zero(T_):
-            return "f2{0.f, 0.f}" if T_ == "f2" else "0.f"
-
+    def vn_col(p, n, j, s, d, final):
+        """VN (or final posterior) of column j (n-th register column of part p) for every lane copy at
+        once: the copies' chains are emitted interleaved, so consecutive adds never depend on each other.
+        Each chain is the reference's sequential fp32 order: S_k = ((P_{k-1} + c_{k+1}) + ...) + c_{d-1},
+        v2c_k = x0 + S_k, P_k = P_{k-1} + c_k (the chains start from the reference's explicit 0)."""
+        grp = [(f"cs{i}", f"xs{i}[{n}]", f"s{i}") for i in range(Q)]
         w(f"        {{  // column {j}, degree {d}")
-        if XPRE:  # the posterior's channel values (cumulative VN weights: xa from memory) issued first
-            for i in range(NP(p)):
-                w(f"            const f2 xl_{i} = (KIND != NLDPC_NEURAL && a.w_vn) ? f2{{bload(xr, vo, {X(j, 2 * i)}), "
-                  f"bload(xr, vo, {X(j, 2 * i + 1)})}} : xp{i}[{n}];")
-            for i in range(NS(p)):
-                w(f"            const float xl_s{i} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, 2 * NP(p) + i)}) : xs{i}[{n}];")
-        for T_, arr, xin, g in grp:
-            w(f"            {T_} P_{g} = {zero(T_)};")
-        if not final:
-            for T_, arr, xin, g in grp:
-                ch = f"chan2<KIND>({xin}, a)" if T_ == "f2" else f"chan<KIND>({xin}, a)"
-                w(f"            const {T_} x0_{g} = {add(T_, zero(T_), ch) if ZADD else ch};")
-            def sub(T_, x, y):
-                return f"({x} - {y})" if T_ == "f2" else f"__fsub_rn({x}, {y})"
-            if QEXACT:  # QMS: exact sums on the quantiser's grid (see QEXACT)
-                w("            if constexpr (KIND == NLDPC_QMS) {")
-                for k in range(d):
-                    for T_, arr, xin, g in grp:
-                        pk = f"{arr}[{s + k}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k}]')
-                        w(f"                P_{g} = {pk};")
-                for T_, arr, xin, g in grp:
-                    w(f"                const {T_} tq_{g} = {add(T_, f'x0_{g}', f'P_{g}')};")
-                for k in range(d):
-                    for T_, arr, xin, g in grp:
-                        w(f"                {arr}[{s + k}] = {sub(T_, f'tq_{g}', f'{arr}[{s + k}]')};")
-                w("            } else {")
-            # edges two at a time: the chains of k and k+1 (S_k from P_{k-1}, S_{k+1} from P_k) run
-            # interleaved -- twice the independent adds per wave for the VN's dependent-add tail.
-            # Chain k reads c_{k+1} first, before chain k+1 overwrites it with v2c_{k+1}.
-            def pairs(k_from, d_, out, ind="            "):
-                """Chains k_from .. d_-1 over c_{k+1} .. c_{d_-1} from the running prefix P; out(g, v) forms
-                what a chain's register receives (v2c = x0 + S, or the partial sum itself)."""
-                for k in range(k_from, d_, 2):
-                    two = k + 1 < d_
-                    w(f"{ind}{{")
-                    if two:
-                        for T_, arr, xin, g in grp:
-                            pk = f"{arr}[{s + k}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k}]')
-                            w(f"{ind}    const {T_} Pk_{g} = {pk};  // P_k")
-                        for T_, arr, xin, g in grp:
-                            s1 = f"{arr}[{s + k + 1}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k + 1}]')
-                            w(f"{ind}    {T_} S_{g} = {s1};")
-                            w(f"{ind}    {T_} U_{g} = Pk_{g};")
-                        for m in range(k + 2, d_):
-                            for T_, arr, xin, g in grp:
-                                w(f"{ind}    S_{g} = {add(T_, f'S_{g}', f'{arr}[{s + m}]')};")
-                                w(f"{ind}    U_{g} = {add(T_, f'U_{g}', f'{arr}[{s + m}]')};")
-                        for T_, arr, xin, g in grp:
-                            w(f"{ind}    const {T_} o_{g} = {arr}[{s + k + 1}];")
-                            w(f"{ind}    {arr}[{s + k}] = {out(T_, g, f'S_{g}')}; "
-                              f"{arr}[{s + k + 1}] = {out(T_, g, f'U_{g}')};")
-                        # the fake dependence of the running prefix on the new messages keeps the compiler
-                        # from running the prefix chain ahead and holding every partial sum in a register
-                        for T_, arr, xin, g in grp:
-                            w(f"{ind}    asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]), \"v\"({arr}[{s + k + 1}]));")
-                        for T_, arr, xin, g in grp:
-                            w(f"{ind}    P_{g} = {add(T_, f'Pk_{g}', f'o_{g}')};")
-                    else:
-                        for T_, arr, xin, g in grp:
-                            w(f"{ind}    {T_} S_{g} = P_{g};")
-                        for T_, arr, xin, g in grp:
-                            w(f"{ind}    const {T_} o_{g} = {arr}[{s + k}]; {arr}[{s + k}] = {out(T_, g, f'S_{g}')};")
-                        for T_, arr, xin, g in grp:
-                            w(f"{ind}    asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]));")
-                        for T_, arr, xin, g in grp:
-                            w(f"{ind}    P_{g} = {add(T_, f'P_{g}', f'o_{g}')};")
-                    w(f"{ind}}}")
-
-            v2c = lambda T_, g, v: add(T_, f"x0_{g}", v)  # noqa: E731
-            m_ = early_m(j)
-            if early:
-                w("            if constexpr (EARLY_VN) {")
-                # EARLYVN late part: chains k < m continue from E_k (their registers) over c_m .. c_{d-1} --
-                # all of them before the chains k >= m overwrite c_m ..; then the prefix continues from P_{m-1}
-                for k in range(0, m_, 2):
-                    two = k + 1 < m_
-                    w("                {")
-                    for T_, arr, xin, g in grp:
-                        w(f"                    {T_} S_{g} = {arr}[{s + k}];")
-                        if two:
-                            w(f"                    {T_} U_{g} = {arr}[{s + k + 1}];")
-                    for m in range(m_, d):
-                        for T_, arr, xin, g in grp:
-                            w(f"                    S_{g} = {add(T_, f'S_{g}', f'{arr}[{s + m}]')};")
-                            if two:
-                                w(f"                    U_{g} = {add(T_, f'U_{g}', f'{arr}[{s + m}]')};")
-                    for T_, arr, xin, g in grp:
-                        w(f"                    {arr}[{s + k}] = {v2c(T_, g, f'S_{g}')};")
-                        if two:
-                            w(f"                    {arr}[{s + k + 1}] = {v2c(T_, g, f'U_{g}')};")
-                    w("                }")
-                for T_, arr, xin, g in grp:
-                    w(f"                P_{g} = pe{g[1:]}[{n}];")
-                pairs(m_, d, v2c, "                ")
-                w("            } else {")
-            pairs(0, d, v2c)
-            if early:
-                w("            }")
-            if QEXACT:
-                w("            }")
-        else:
+        for arr, xin, g in grp:
+            w(f"            float P_{g} = 0.f;")
+        if final:
             for k in range(d):
-                for T_, arr, xin, g in grp:
-                    pk = f"{arr}[{s + k}]" if k == 0 and not ZADD else add(T_, f'P_{g}', f'{arr}[{s + k}]')
-                    w(f"            P_{g} = {pk};")
+                for arr, xin, g in grp:
+                    w(f"            P_{g} = fadd(P_{g}, {arr}[{s + k}]);")
+            return
+        for arr, xin, g in grp:
+            w(f"            const float x0_{g} = fadd(0.f, chan<KIND>({xin}, a));")
+        # QMS: every VN input lies on the quantiser's 0.5 grid with |x| <= 15.5, so every partial sum of a
+        # column (<= 24 terms) is exact in fp32 and the reference's sequential S_k equals (x0 + C) - c_k bit
+        # for bit (C = the posterior's own sum): d + 1 adds per column copy instead of d(d-1)/2 + d (QEXACT)
+        w("            if constexpr (KIND == NLDPC_QMS) {")
+        for k in range(d):
+            for arr, xin, g in grp:
+                w(f"                P_{g} = fadd(P_{g}, {arr}[{s + k}]);")
+        for arr, xin, g in grp:
+            w(f"                const float tq_{g} = fadd(x0_{g}, P_{g});")
+        for k in range(d):
+            for arr, xin, g in grp:
+                w(f"                {arr}[{s + k}] = __fsub_rn(tq_{g}, {arr}[{s + k}]);")
+        w("            } else {")
+        # edges two at a time: the chains of k and k+1 (S_k from P_{k-1}, S_{k+1} from P_k) run interleaved --
+        # twice the independent adds per wave for the VN's dependent-add tail.  Chain k reads c_{k+1} first,
+        # before chain k+1 overwrites it with v2c_{k+1}.
+        ind = "            "
+        for k in range(0, d, 2):
+            w(f"{ind}{{")
+            if k + 1 < d:
+                for arr, xin, g in grp:
+                    w(f"{ind}    const float Pk_{g} = fadd(P_{g}, {arr}[{s + k}]);  // P_k")
+                for arr, xin, g in grp:
+                    w(f"{ind}    float S_{g} = fadd(P_{g}, {arr}[{s + k + 1}]);")
+                    w(f"{ind}    float U_{g} = Pk_{g};")
+                for m in range(k + 2, d):
+                    for arr, xin, g in grp:
+                        w(f"{ind}    S_{g} = fadd(S_{g}, {arr}[{s + m}]);")
+                        w(f"{ind}    U_{g} = fadd(U_{g}, {arr}[{s + m}]);")
+                for arr, xin, g in grp:
+                    w(f"{ind}    const float o_{g} = {arr}[{s + k + 1}];")
+                    w(f"{ind}    {arr}[{s + k}] = fadd(x0_{g}, S_{g}); {arr}[{s + k + 1}] = fadd(x0_{g}, U_{g});")
+                # the fake dependence of the running prefix on the new messages keeps the compiler from
+                # running the prefix chain ahead and holding every partial sum in a register
+                for arr, xin, g in grp:
+                    w(f"{ind}    asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]), \"v\"({arr}[{s + k + 1}]));")
+                for arr, xin, g in grp:
+                    w(f"{ind}    P_{g} = fadd(Pk_{g}, o_{g});")
+            else:
+                for arr, xin, g in grp:
+                    w(f"{ind}    float S_{g} = P_{g};")
+                for arr, xin, g in grp:
+                    w(f"{ind}    const float o_{g} = {arr}[{s + k}]; {arr}[{s + k}] = fadd(x0_{g}, S_{g});")
+                for arr, xin, g in grp:
+                    w(f"{ind}    asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s + k}]));")
+                for arr, xin, g in grp:
+                    w(f"{ind}    P_{g} = fadd(P_{g}, o_{g});")
+            w(f"{ind}}}")
+        w("            }")
 
     for p in range(S.P):
         cols = S.reg_cols[p]
@@ -617,64 +501,34 @@ def emit(S: Spec) -> str:
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void {fname}({state_params(p)}, {x_params(p)}, const FusedArgs& a, "
               f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t* appw, int u, "
-              f"uint32_t d1m, rsrc_t apr{pe_params(p)}) {{")
+              f"const uint32_t (&d1m)[{nwords(p, 'd1m')}], rsrc_t apr) {{")
             if not final:
                 w("    const bool ucn_ = KIND != NLDPC_NEURAL && a.ucn;  // UCN: hard decisions of the previous posterior")
-            if XPRE2 and NP(p) == 0:
-                # every posterior's xa (cumulative VN weights) requested before the first posterior store:
-                # a later load would wait (vmcnt counts in order) for every store issued before it
-                for n, j in enumerate(cols):
-                    for i in range(NS(p)):
-                        w(f"    const float xl_{n}_{i} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, i)}) : xs{i}[{n}];")
+            # every posterior's xa (cumulative VN weights) requested before the first posterior store: a later
+            # load would wait (vmcnt counts loads and stores in order) for every store issued before it (XPRE)
+            for n, j in enumerate(cols):
+                for i in range(Q):
+                    w(f"    const float xl_{n}_{i} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, i)}) : xs{i}[{n}];")
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
-                vn_col(p, n, j, s, d, final, early=not final and early_m(j) >= 2)
-                for i in range(NP(p)):
+                vn_col(p, n, j, s, d, final)
+                for q in range(Q):
                     w("            {")
-                    if XPRE:
-                        w(f"            const f2 xo_ = xl_{i};")
-                    else:
-                        w(f"            const f2 xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? f2{{bload(xr, vo, {X(j, 2 * i)}), "
-                          f"bload(xr, vo, {X(j, 2 * i + 1)})}} : xp{i}[{n}];")
-                    w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
-                    w("                bool m0_, m1_;")
-                    w(f"                bstore(pr, vo, {X(j, 2 * i)}, posterior_m<KIND>(xo_.x, P_{i}.x, a, m0_));")
-                    w(f"                bstore(pr, vo, {X(j, 2 * i + 1)}, posterior_m<KIND>(xo_.y, P_{i}.y, a, m1_));")
-                    w(f"                bstore8(pm, vm, {X(j, 2 * i) // 4}, m0_);")
-                    w(f"                bstore8(pm, vm, {X(j, 2 * i + 1) // 4}, m1_);")
-                    w("            } else {")
-                    w(f"                const f2 y_ = posterior2<KIND>(xo_, P_{i}, a);")
-                    w(f"                put_post<CM>(pr, vo, {X(j, 2 * i)}, y_.x, ps);")
-                    w(f"                put_post<CM>(pr, vo, {X(j, 2 * i + 1)}, y_.y, ps);")
-                    w("            }")
-                    w("            }")
-                for i in range(NS(p)):
-                    q = 2 * NP(p) + i
-                    w("            {")
-                    w(f"            const float xo_ = xl_s{i};" if XPRE else
-                      f"            const float xo_ = xl_{n}_{i};" if (XPRE2 and NP(p) == 0) else
-                      f"            const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : xs{i}[{n}];")
+                    w(f"            const float xo_ = xl_{n}_{q};")
                     w("            float y_;")
                     w("            if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w("                bool m_;")
-                    w(f"                y_ = posterior_m<KIND>(xo_, P_s{i}, a, m_);")
+                    w(f"                y_ = posterior_m<KIND>(xo_, P_s{q}, a, m_);")
                     w(f"                bstore(pr, vo, {X(j, q)}, y_);")
                     w(f"                bstore8(pm, vm, {X(j, q) // 4}, m_);")
                     w("            } else {")
-                    w(f"                y_ = posterior<KIND>(xo_, P_s{i}, a);")
+                    w(f"                y_ = posterior<KIND>(xo_, P_s{q}, a);")
                     w(f"                put_post<CM>(pr, vo, {X(j, q)}, y_, ps);")
                     w("            }")
                     if not final:
-                        app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xs{i}[{n}], a))"
-                        b_ = f"(it == 0 ? {app0} : y_) >= 0.f"
-                        if S.ucn_bw:
-                            w(f"            if (ucn_) app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {b_});")
-                        elif S.ucn_wave:
-                            w(f"            if (ucn_) {{ if constexpr (UCNW) app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {b_}); "
-                              f"else app_or(appw, {j * S.WZX}, u + {q * ZT}, {b_}); }}")
-                        else:
-                            w(f"            if (ucn_) app_or(appw, {j * S.WZX}, u + {q * ZT}, {b_});")
+                        app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xs{q}[{n}], a))"
+                        w(f"            if (ucn_) app_or(appw, {j * S.WZX}, u + {q * ZT}, (it == 0 ? {app0} : y_) >= 0.f);")
                     w("            }")
                 w("        }")
                 w("        __builtin_amdgcn_sched_barrier(0);")
@@ -686,66 +540,9 @@ def emit(S: Spec) -> str:
                 for n, j in enumerate(S.d1_cols[p]):
                     for q in range(Q):
                         app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xd[{n * Q + q}], a))"
-                        bit = f"it == 0 ? {app0} >= 0.f : ((d1m >> {n * Q + q}) & 1u) != 0u"
-                        if S.ucn_bw:
-                            w(f"        app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {bit});")
-                        elif S.ucn_wave:
-                            w(f"        if constexpr (UCNW) app_wave<{S.WZ}>(appw + {j * S.WZX}, u + {q * ZT}, {bit}); "
-                              f"else app_or(appw, {j * S.WZX}, u + {q * ZT}, {bit});")
-                        else:
-                            w(f"        app_or(appw, {j * S.WZX}, u + {q * ZT}, {bit});")
+                        bit = f"it == 0 ? {app0} >= 0.f : ({bit_get('d1m', n * Q + q)} & 1u) != 0u"
+                        w(f"        app_or(appw, {j * S.WZX}, u + {q * ZT}, {bit});")
                 w("    }")
-            w("}")
-
-    # EARLYVN early part: for each column's edges k < m (chunks 0-1), E_k = ((P_{k-1} + c_{k+1}) + ...) + c_{m-1}
-    # replaces c_k (read by no later sum), the prefix P_{m-1} goes to pe -- the same operations, in the same
-    # order, as the first steps of vn_col's chains (pairs of chains interleaved as there)
-    if EVN:
-        for p in range(S.P):
-            w("template <int KIND, int MODE>")
-            w(f"__device__ __forceinline__ void vne_p{p}({state_params(p)}{pe_params(p)}) {{")
-            s_ = 0
-            for n, j in enumerate(S.reg_cols[p]):
-                d, m_ = len(S.col_edges[j]), early_m(j)
-                if m_ >= 2:
-                    gs = [(f"cs{i}", f"s{i}", i) for i in range(NS(p))]
-                    w(f"    {{  // column {j}: edges 0..{m_ - 1} of {d}")
-                    for arr, g, i in gs:
-                        w(f"        float P_{g} = 0.f;")
-                    for k in range(0, m_, 2):
-                        two = k + 1 < m_
-                        w("        {")
-                        if two:
-                            for arr, g, i in gs:
-                                pk = f"{arr}[{s_ + k}]" if k == 0 and not ZADD else f"fadd(P_{g}, {arr}[{s_ + k}])"
-                                w(f"            const float Pk_{g} = {pk};")
-                            for arr, g, i in gs:
-                                s1 = f"{arr}[{s_ + k + 1}]" if k == 0 and not ZADD else f"fadd(P_{g}, {arr}[{s_ + k + 1}])"
-                                w(f"            float S_{g} = {s1};")
-                                w(f"            float U_{g} = Pk_{g};")
-                            for mm in range(k + 2, m_):
-                                for arr, g, i in gs:
-                                    w(f"            S_{g} = fadd(S_{g}, {arr}[{s_ + mm}]);")
-                                    w(f"            U_{g} = fadd(U_{g}, {arr}[{s_ + mm}]);")
-                            for arr, g, i in gs:
-                                w(f"            const float o_{g} = {arr}[{s_ + k + 1}];")
-                                w(f"            {arr}[{s_ + k}] = S_{g}; {arr}[{s_ + k + 1}] = U_{g};")
-                            for arr, g, i in gs:
-                                w(f"            asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s_ + k}]), \"v\"({arr}[{s_ + k + 1}]));")
-                            for arr, g, i in gs:
-                                w(f"            P_{g} = fadd(Pk_{g}, o_{g});")
-                        else:
-                            for arr, g, i in gs:
-                                w(f"            const float o_{g} = {arr}[{s_ + k}]; {arr}[{s_ + k}] = P_{g};")
-                            for arr, g, i in gs:
-                                w(f"            asm volatile(\"\" : \"+v\"(P_{g}) : \"v\"({arr}[{s_ + k}]));")
-                            for arr, g, i in gs:
-                                w(f"            P_{g} = fadd(P_{g}, o_{g});")
-                        w("        }")
-                    for arr, g, i in gs:
-                        w(f"        pe{i}[{n}] = P_{g};")
-                    w("    }")
-                s_ += d
             w("}")
 
     # ---------------------------------------------------------------- LDS chunk write / read-back
@@ -754,114 +551,58 @@ def emit(S: Spec) -> str:
         check copy h = (v - s_e) mod Z of the chunk's check-ordered image.  Only one of the Q copies
         of a shifted edge can wrap inside the lane range; the others are a constant offset."""
         cq = (q * ZT - int(S.shift[e])) % Z
-        base = (e - e0) * Z + cq
+        base = (S.slot[e] - e0) * Z + cq
         if cq + ZT <= Z:
             return f"{base} + u"
         return f"{base} + u - (u >= {Z - cq} ? {Z} : 0)"
 
     def own_lv(e, q, e0):
-        """The LDS element own() indexes, as an lvalue.  WRAPM: a wrapped copy's lanes pick between two
-        per-thread byte bases (lu0_, lu1_ = lu0_ - 4Z) by a lane mask the scalar unit computes from the
-        wave's first copy (wrap_mask), one v_cndmask instead of a compare, a select and an add."""
-        cq = (q * ZT - int(S.shift[e])) % Z
-        base = (e - e0) * Z + cq
-        if cq + ZT <= Z or not WRAPM:
-            return f"lds[{own(e, q, e0)}]"
-        return (f"((lds_fp)(uintptr_t)((__builtin_amdgcn_inverse_ballot_w64(wrap_mask({Z - cq}, u0_)) ? lu1_ : lu0_) "
-                f"+ {4 * base}u))[0]")
-
-    def own_tid_write(e, q, e0, val):
-        """OWNTID: the owner's LDS write of (edge e, lane copy q) by ds_write_addtid_b32 at M0 = the wave's
-        LDS base (lane 0's copy) + the slot; a wrapped copy (lanes u >= T go Z slots back) writes twice,
-        lanes u < T and u >= T under their own EXEC (wrap_mask from the wave's first copy), EXEC restored."""
-        cq = (q * ZT - int(S.shift[e])) % Z
-        base = (e - e0) * Z + cq
-        w("    {")
-        if cq + ZT <= Z:
-            w(f"        asm volatile(\"s_mov_b32 m0, %0\\n\\ts_nop 0\\n\\tds_write_addtid_b32 %1\" :: \"s\"(slu_ + {4 * base}u), "
-              f"\"v\"({val}) : \"memory\", \"m0\");")
-        else:
-            w(f"        const uint64_t wm_ = wrap_mask({Z - cq}, su0_);  // lanes that wrap")
-            w("        uint64_t sv_;")
-            w("        asm volatile(\"s_mov_b64 %0, exec\\n\\ts_andn2_b64 exec, %0, %1\\n\\ts_mov_b32 m0, %2\\n\\ts_nop 0\\n\\t"
-              "ds_write_addtid_b32 %4\\n\\ts_and_b64 exec, %0, %1\\n\\ts_mov_b32 m0, %3\\n\\ts_nop 0\\n\\t"
-              "ds_write_addtid_b32 %4\\n\\ts_mov_b64 exec, %0\\n\\ts_nop 0\" : \"=&s\"(sv_) : \"s\"(wm_), "
-              f"\"s\"(slu_ + {4 * base}u), \"s\"(slu_ + {(4 * (base - Z)) & 0xFFFFFFFF}u), \"v\"({val}) : \"memory\", \"m0\");")
-        w("    }")
-
-    def wrap_u0():  # before the asm barrier on u, so the compiler computes it once, not per phase
-        if WRAPM:
-            w("    const int u0_ = __builtin_amdgcn_readfirstlane(u) & ~63;  // the wave's first lane copy")
-
-    def wrap_prelude():
-        if WRAPM:
-            w("    const uint32_t lu0_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u, lu1_ = lu0_ - "
-              f"{4 * Z}u;")
+        return f"lds[{own(e, q, e0)}]"
 
     for p in range(S.P):
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
-            mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
-            d1 = [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
+            mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= S.slot[e] < e1]
+            # (compacted image: the degree-1 edges have no slot -- D1_BYPASS holds for every kind there)
+            d1 = [] if S.compact else [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void wr_p{p}_c{ci}({state_params(p, True)}, {x_params(p)}, float* lds, "
               f"int u, const FusedArgs& a, int it, rsrc_t sv, uint32_t vc) {{")
-            wrap_u0()
-            if OWNTID and S.ZT % 64 == 0 and not S.padded and SAVECOPY:  # the wave's first copy and its LDS base
-                w("    const int su0_ = __builtin_amdgcn_readfirstlane(u);")
-                w("    const uint32_t slu_ = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u);")
             w("    asm volatile(\"\" : \"+v\"(u));  // LDS addresses are recomputed here, not hoisted out of the loop")
-            wrap_prelude()
             for q in range(Q):
                 for k, e in mine:
-                    cq_ = (q * ZT - int(S.shift[e])) % Z
-                    if OWNTID and S.ZT % 64 == 0 and not S.padded and SAVECOPY and not (
-                            OWNTID_MODE == 2 and cq_ + ZT > Z) and not (OWNTID_MODE == 3 and cq_ + ZT <= Z):
-                        own_tid_write(e, q, e0, ref(p, q, k))
-                        continue
                     w(f"    {own_lv(e, q, e0)} = {ref(p, q, k)};")
-                    if not SAVECOPY:
-                        w(f"    if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, {ref(p, q, k)}, a.qp);")
             if d1:  # v2c = (0 + xin) + 0: no other edge in the column (bypass: the check node reads xa)
                 w("    if constexpr (!D1_BYPASS) {")
             for j, e in d1:
                 for q in range(Q):
-                    v1 = f"fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f)" if ZADD else f"chan<KIND>({xref(p, j, q)}, a)"
-                    w(f"    {{ const float v_ = {v1}; "
-                      f"{own_lv(e, q, e0)} = v_; " +
-                      ("}" if SAVECOPY else f"if constexpr (SAVE) save_v2c<KIND>(sv, vc, {e * Z + q * ZT}, v_, a.qp); }}"))
+                    w(f"    {{ const float v_ = fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f); {own_lv(e, q, e0)} = v_; }}")
             if d1:
                 w("    }")
             w("}")
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
               f"int u, const FusedArgs& a, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co, "
-              f"uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t& d1m) {{")
-            wrap_u0()
+              f"uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t (&d1m)[{nwords(p, 'd1m')}]) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
-            wrap_prelude()
             for q in range(Q):
                 for k, e in mine:
                     w(f"    {ref(p, q, k)} = {own_lv(e, q, e0)};")
             if d1:  # this iteration's posterior right away (bypass: written by the check node)
                 w("    if constexpr (!D1_BYPASS) {")
-            if XPRE2:
-                for j, e in d1:
-                    for q in range(Q):
-                        w(f"    const float xl_{j}_{q} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
+            for j, e in d1:
+                for q in range(Q):
+                    w(f"    const float xl_{j}_{q} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
             for j, e in d1:
                 for q in range(Q):
                     bit = S.d1_cols[p].index(j) * Q + q
-                    if XPRE2:
-                        w(f"    {{ const float xo_ = xl_{j}_{q};")
-                    else:
-                        w(f"    {{ const float xo_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
-                    w(f"      const float P_ = {'fadd(0.f, ' + own_lv(e, q, e0) + ')' if ZADD else own_lv(e, q, e0)};")
+                    w(f"    {{ const float xo_ = xl_{j}_{q};")
+                    w(f"      const float P_ = fadd(0.f, {own_lv(e, q, e0)});")
                     w("      float y_;")
                     w("      if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
                     w(f"          bool m_; y_ = posterior_m<KIND>(xo_, P_, a, m_); bstore(pr, vo, {X(j, q)}, y_); "
                       f"bstore8(pm, vm, {X(j, q) // 4}, m_);")
                     w(f"      }} else {{ y_ = posterior<KIND>(xo_, P_, a); put_post<CM>(pr, vo, {X(j, q)}, y_, ps); }}")
-                    w(f"      if (KIND != NLDPC_NEURAL && a.ucn) d1m = (d1m & ~(1u << {bit})) | ((y_ >= 0.f ? 1u : 0u) << {bit}); }}")
+                    w(f"      if (KIND != NLDPC_NEURAL && a.ucn) {bit_set('d1m', bit, 'y_ >= 0.f')}; }}")
             if d1:
                 w("    if (has_co) {  // final message state (last iteration only)")
                 for j, e in d1:
@@ -896,12 +637,10 @@ def emit(S: Spec) -> str:
             S.cn_order[(p, ci)] = list(dict.fromkeys(i for i, _ in S.cn_units[ci][p]))  # distinct rows, unit order
             S.cn_nw[(p, ci)] = max(sum(len(S.row_edges[i]) for i in S.cn_order[(p, ci)]), 1)
 
-    def rot(e, q, mask=False):  # check copy h = u + q*ZT of edge e sits at variable copy (u + c) mod Z
+    def rot(e, q):  # check copy h = u + q*ZT of edge e sits at variable copy (u + c) mod Z
         c = (q * ZT + int(S.shift[e])) % Z
         if c + ZT <= Z:
             return c, "0u"
-        if mask and WRAPM:  # (check-node phase: u0_ defined, see own_lv)
-            return c, f"(__builtin_amdgcn_inverse_ballot_w64(wrap_mask({Z - c}, u0_)) ? {(-4 * Z) & 0xFFFFFFFF}u : 0u)"
         return c, f"(u >= {Z - c} ? {(-4 * Z) & 0xFFFFFFFF}u : 0u)"
 
     for p in range(S.P):
@@ -911,150 +650,96 @@ def emit(S: Spec) -> str:
             w(f"__device__ __forceinline__ void cn_p{p}_c{ci}(float* lds, int u, const FusedArgs& a, int it, "
               f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last, "
               f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps, "
-              f"const uint32_t* appw, rsrc_t xr, rsrc_t apr, uint32_t& cdm) {{")
-            wrap_u0()
+              f"const uint32_t* appw, rsrc_t xr, rsrc_t apr, uint32_t (&cdm)[{nwords(p, 'cdm')}]) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
-            if ROADDR:
-                w("    const uint32_t lu_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u;")
-            tid = CNTID and S.ZT % 64 == 0 and not S.padded
-            if tid:  # the wave's copies are u0 + lane: its LDS base is lane 0's (M0 for ds_write_addtid_b32)
-                w("    const uint32_t slu_ = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u);")
+            w("    const uint32_t lu_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u;")
             # row copies in order; weight offsets of each row in the preloaded W/Bv arrays
             rcs, woff, wo = list(S.cn_units[ci][p]), {}, 0
             for i in S.cn_order[(p, ci)]:
                 woff[i] = wo
                 wo += len(S.row_edges[i])
 
+            def row_slots(i):
+                """The row's first LDS slot and each slotted edge's float offset from it (compacted image: the
+                row's slots are consecutive, its degree-1 edges have none)."""
+                es = S.row_edges[i]
+                rb = min((S.slot[e] for e in es if e in S.slot), default=e0c)
+                return rb, {e: (S.slot[e] - rb) * Z for e in es if e in S.slot}
+
             def rc_load(n):
                 i, q = rcs[n]
                 es = S.row_edges[i]
-                DC, e0 = len(es), es[0]
+                DC = len(es)
+                e0, off = row_slots(i)
                 w(f"    float m{n}[{DC}];  // row {i} copy {q}")
-                if ROADDR:  # the row copy's LDS byte address = lu_ + constant: one v_add_u32 (ROA kinds)
-                    w(f"    std::conditional_t<ROA, lds_fp, float*> rq{n};")
-                    w("    if constexpr (ROA) {")
-                    w(f"        uint32_t rb = lu_ + {4 * ((e0 - e0c) * Z + q * ZT)}u;")
-                    w("        asm volatile(\"\" : \"+v\"(rb));")
-                    w(f"        rq{n} = (decltype(rq{n}))(uintptr_t)rb;")
-                    w("    } else {")
-                    w(f"        int ro = {(e0 - e0c) * Z + q * ZT} + u;")
-                    w("        asm volatile(\"\" : \"+v\"(ro));")
-                    w(f"        rq{n} = (decltype(rq{n}))(lds + ro);")
-                    w("    }")
-                else:
-                    w(f"    float* rq{n};")
-                    w("    {")
-                    w(f"        int ro = {(e0 - e0c) * Z + q * ZT} + u;  // one base VGPR per row copy: the edges ride in")
-                    if not NORO:
-                        w("        asm volatile(\"\" : \"+v\"(ro));  // the 16-bit DS offset")
-                    w(f"        rq{n} = lds + ro;")
-                    w("    }")
+                # the row copy's LDS byte address = lu_ + constant: one v_add_u32 (ROA kinds); the edges ride
+                # in the 16-bit DS offset
+                w(f"    std::conditional_t<ROA, lds_fp, float*> rq{n};")
+                w("    if constexpr (ROA) {")
+                w(f"        uint32_t rb = lu_ + {4 * ((e0 - e0c) * Z + q * ZT)}u;")
+                w("        asm volatile(\"\" : \"+v\"(rb));")
+                w(f"        rq{n} = (decltype(rq{n}))(uintptr_t)rb;")
+                w("    } else {")
+                w(f"        int ro = {(e0 - e0c) * Z + q * ZT} + u;")
+                w("        asm volatile(\"\" : \"+v\"(ro));")
+                w(f"        rq{n} = (decltype(rq{n}))(lds + ro);")
+                w("    }")
                 for k, e in enumerate(es):
                     if e in d1set:
-                        w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = d1_v2c<KIND, {1 if ZADD else 0}>(cd[{S.cd_index[p].index((e, q))}], a); "
-                          f"else m{n}[{k}] = rq{n}[{k * Z}];")
+                        if S.compact:
+                            w(f"    m{n}[{k}] = d1_v2c<KIND, 1>(cd[{S.cd_index[p].index((e, q))}], a);")
+                        else:
+                            w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = d1_v2c<KIND, 1>(cd[{S.cd_index[p].index((e, q))}], a); "
+                              f"else m{n}[{k}] = rq{n}[{off[e]}];")
                     elif "cnread" in SKIP:  # (timing experiment: no check-node LDS reads, junk inputs)
                         w(f"    m{n}[{k}] = __uint_as_float(0x3f800000u + ((uint32_t)u << 8) + {k * 977 + n * 131}u);")
                     else:
-                        w(f"    m{n}[{k}] = rq{n}[{k * Z}];")
+                        w(f"    m{n}[{k}] = rq{n}[{off[e]}];")
 
             def rc_compute(n):
                 i, q = rcs[n]
                 es = S.row_edges[i]
                 DC = len(es)
-                if S.ucn_wave and (n == 0 or rcs[n - 1][0] != i):  # the row's first unit in this part
-                    # the row's unsatisfied flags for this wave's copies, all Q of them at once: lane 2q+h
-                    # XORs the 32-bit windows (copies u0 + q*ZT + 32h + 0..31, rotated by each edge's shift)
-                    # of the row's columns; the 2Q words become Q lane masks (bit l = lane l's flag)
-                    w(f"    uint64_t {', '.join(f'umr{i}_{qq} = 0' for qq in range(Q))};")
-                    w("    if (UCNW && a.ucn) {")
-                    w("        const int l_ = threadIdx.x & 63;")
-                    w(f"        const uint32_t bq_ = (uint32_t)(u - l_ + min(l_ >> 1, {Q - 1}) * {ZT} + (l_ & 1) * 32);")
-                    w(f"        uint32_t wl_[{DC}], wh_[{DC}], sh_[{DC}];  // all windows' words requested first")
-                    for k, e in enumerate(es):
-                        j = int(S.hb_cols[e])
-                        w(f"        app_win_load(appw + {j * S.WZX}, bq_ + {int(S.shift[e])}u, {Z}u, wl_[{k}], wh_[{k}], sh_[{k}]);")
-                    w("        uint32_t pw_ = 0u;")
-                    w(f"        for (int k = 0; k < {DC}; ++k) pw_ ^= __builtin_amdgcn_alignbit(wh_[k], wl_[k], sh_[k]);")
-                    for qq in range(Q):
-                        w(f"        umr{i}_{qq} = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(pw_, {2 * qq + 1}) << 32) | "
-                          f"(uint32_t)__builtin_amdgcn_readlane(pw_, {2 * qq});")
-                    w("    }")
+                _, off = row_slots(i)
                 w("    {")
                 w(f"        float wv[{DC}], bv[{DC}];")
                 w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{woff[i]} + k]; bv[k] = Bv[{woff[i]} + k]; }}")
                 w("        const bool wc = a.w_cn != nullptr;")
                 w("        float uf_ = 0.f;  // UCN: unsatisfied check (odd number of row variables with APP >= 0)")
                 w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
-                if S.ucn_wave:
-                    w(f"            if constexpr (UCNW) uf_ = __builtin_amdgcn_inverse_ballot_w64(umr{i}_{q}) ? 1.f : 0.f;")
-                    w("            else {")
                 w("            uint32_t par_ = 0;")
-                if UCNB:  # every word of the row requested first, then the shifts and XORs (one LDS wait, not DC)
-                    ks = [(k, e) for k, e in enumerate(es) if e not in d1set]
-                    for k, e in ks:
-                        c, dvu = rot(e, q)
-                        j = int(S.hb_cols[e])
-                        # (u + c) mod Z as min(v, v - Z) on unsigned: v - Z wraps above v unless v >= Z
-                        vexpr = f"(uint32_t)u + {c}u" if c + ZT <= Z else f"min((uint32_t)u + {c}u, (uint32_t)u + {c - Z}u)"
-                        w(f"            const uint32_t v{k}_ = {vexpr}; const uint32_t w{k}_ = appw[{j * S.WZX} + (v{k}_ >> 5)];")
-                    for k, e in ks:
-                        w(f"            par_ ^= w{k}_ >> (v{k}_ & 31u);")
+                # every word of the row requested first, then the shifts and XORs (one LDS wait, not DC; UCNB)
+                ks = [(k, e) for k, e in enumerate(es) if e not in d1set]
+                for k, e in ks:
+                    c, dvu = rot(e, q)
+                    j = int(S.hb_cols[e])
+                    # (u + c) mod Z as min(v, v - Z) on unsigned: v - Z wraps above v unless v >= Z
+                    vexpr = f"(uint32_t)u + {c}u" if c + ZT <= Z else f"min((uint32_t)u + {c}u, (uint32_t)u + {c - Z}u)"
+                    w(f"            const uint32_t v{k}_ = {vexpr}; const uint32_t w{k}_ = appw[{j * S.WZX} + (v{k}_ >> 5)];")
+                for k, e in ks:
+                    w(f"            par_ ^= w{k}_ >> (v{k}_ & 31u);")
                 for k, e in enumerate(es):
+                    if e not in d1set:
+                        continue
                     c, dvu = rot(e, q)
                     j = int(S.hb_cols[e])
                     vexpr = f"u + {c}" if c + ZT <= Z else f"u + {c} - (u >= {Z - c} ? {Z} : 0)"
                     rd_ = f"{{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZX} + (v_ >> 5)] >> (v_ & 31); }}"
-                    if UCNB and e not in d1set:
-                        continue
-                    if e in d1set:  # bypass: the hard decision of this thread's own previous posterior
-                        ix = S.cd_index[p].index((e, q))
-                        app0 = f"(a.first_iter > 0 ? bload(apr, vo + {dvu}, {4 * (j * Z + c)}) : chan<KIND>(cd[{ix}], a))"
-                        w(f"            if constexpr (D1_BYPASS) par_ ^= it == 0 ? ({app0} >= 0.f ? 1u : 0u) : (cdm >> {ix}); "
-                          f"else {rd_}")
-                    else:
-                        w(f"            {rd_}")
+                    # bypass: the hard decision of this thread's own previous posterior
+                    ix = S.cd_index[p].index((e, q))
+                    app0 = f"(a.first_iter > 0 ? bload(apr, vo + {dvu}, {4 * (j * Z + c)}) : chan<KIND>(cd[{ix}], a))"
+                    w(f"            if constexpr (D1_BYPASS) par_ ^= it == 0 ? ({app0} >= 0.f ? 1u : 0u) : {bit_get('cdm', ix)}; "
+                      f"else {rd_}")
                 w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
-                if S.ucn_wave:
-                    w("            }")
                 w("        }")
-                pair_first = CNPAIR2 and CNPIPE and q == 0 and n + 1 < len(rcs) and rcs[n + 1] == (i, 1)
-                pair_second = CNPAIR2 and CNPIPE and q == 1
-                if "cnmath" in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
-                    pass
-                elif pair_first:  # Neural: copies 0 and 1 of the row together, packed epilogue
-                    w(f"        if constexpr (KIND == NLDPC_NEURAL) neural_row2<{DC}>(m{n}, m{n + 1}, wv, bv);")
-                    w(f"        else cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
-                elif pair_second:
-                    w(f"        if constexpr (KIND != NLDPC_NEURAL) cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
-                else:
+                if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
                     w(f"        cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
-                if tid:  # every non-bypassed edge's c2v by one M0 and ds_write_addtid_b32 per edge
-                    wl = [(k, e) for k, e in enumerate(es) if e not in d1set]
-                    regs = ", ".join(f'"v"(m{n}[{k}])' for k, e in wl)
-                    ins = "\\n\\t".join(f"ds_write_addtid_b32 %{i + 1} offset:{4 * k * Z}" for i, (k, e) in enumerate(wl))
-                    cond = "if constexpr (!D1_BYPASS) " if any(e in d1set for e in es) else ""
-                    w(f"        {{ const uint32_t m0_ = slu_ + {4 * ((es[0] - e0c) * Z + q * ZT)}u;")
-                    if any(e in d1set for e in es):  # (no bypass: the degree-1 edges are written too)
-                        w("          if constexpr (!D1_BYPASS) {")
-                        for k, e in enumerate(es):
-                            if e in d1set:
-                                w(f"            rq{n}[{k * Z}] = m{n}[{k}];")
-                        w("          }")
-                    if wl:
-                        # (s_nop: one wait state between an M0 write and a DS *_ADDTID read of it on gfx9 -- the
-                        # hazard recognizer does not look inside inline asm)
-                        w(f"          asm volatile(\"s_mov_b32 m0, %0\\n\\ts_nop 0\\n\\t{ins}\" :: \"s\"(m0_), {regs} : \"memory\", \"m0\"); }}")
-                    else:
-                        w("        }")
                 for k, e in enumerate(es):
-                    if tid and e not in d1set:
-                        continue
                     if e in d1set:
                         j = int(S.hb_cols[e])
-                        c, dv = rot(e, q, mask=True)
+                        c, dv = rot(e, q)
                         ix = S.cd_index[p].index((e, q))
-                        pm = f"fadd(0.f, m{n}[{k}])" if ZADD else f"m{n}[{k}]"
+                        pm = f"fadd(0.f, m{n}[{k}])"
                         w("        if constexpr (D1_BYPASS) {")
                         w(f"            const uint32_t dv_ = {dv};")
                         w("            float y_;")
@@ -1062,43 +747,36 @@ def emit(S: Spec) -> str:
                         w("            else {  // Boosted: the unweighted channel value (cumulative VN weights: from memory)")
                         w(f"                const float xo_ = a.w_vn ? bload(xr, vo + dv_, {4 * (j * Z + c)}) : cd[{ix}];")
                         w(f"                y_ = posterior<KIND>(xo_, {pm}, a);")
-                        w(f"                if (a.ucn) cdm = (cdm & ~(1u << {ix})) | ((y_ >= 0.f ? 1u : 0u) << {ix});")
+                        w(f"                if (a.ucn) {bit_set('cdm', ix, 'y_ >= 0.f')};")
                         w("            }")
                         if "d1post" in SKIP:  # (timing experiment: no degree-1 posterior stores)
                             w("            asm volatile(\"\" :: \"v\"(y_));")
                         else:
                             w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, y_, ps);")
                         w(f"            if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m{n}[{k}]);")
-                        w(f"        }} else {{ rq{n}[{k * Z}] = m{n}[{k}]; }}")
+                        w("        }" if S.compact else f"        }} else {{ rq{n}[{off[e]}] = m{n}[{k}]; }}")
                     elif "cnwrite" in SKIP:  # (timing experiment: keep the value live without the LDS write)
                         w(f"        asm volatile(\"\" :: \"v\"(m{n}[{k}]));")
                     else:
-                        w(f"        rq{n}[{k * Z}] = m{n}[{k}];")
+                        w(f"        rq{n}[{off[e]}] = m{n}[{k}];")
                 w("    }")
 
-            if CNPIPE:
-                # the next row copy's reads go out before this one computes (its slots are disjoint from
-                # every slot this one writes, so program order already allows it); CNDEPTH row copies ahead
-                for n in range(min(CNDEPTH, len(rcs))):
-                    rc_load(n)
-                for n in range(len(rcs)):
-                    if n + CNDEPTH < len(rcs):
-                        rc_load(n + CNDEPTH)
-                    w("    __builtin_amdgcn_sched_barrier(0);")
-                    rc_compute(n)
-            else:
-                for n in range(len(rcs)):
-                    rc_load(n)
-                    rc_compute(n)
-                    if Q > 1 and len(S.row_edges[rcs[n][0]]) > CN_PAIR_MAXDC:
-                        w("    __builtin_amdgcn_sched_barrier(0);")
+            # the next row copy's reads go out before this one computes (its slots are disjoint from every
+            # slot this one writes, so program order already allows it)
+            if rcs:
+                rc_load(0)
+            for n in range(len(rcs)):
+                if n + 1 < len(rcs):
+                    rc_load(n + 1)
+                w("    __builtin_amdgcn_sched_barrier(0);")
+                rc_compute(n)
             w("}")
 
     # ---------------------------------------------------------------- SAVE: chunk image -> saved v2c
     # The image of chunk c is [G][CF] floats in check order: edge e0+i's message for check copy h at
     # i*Z + h, the saved buffer's layout for this codeword's edges e0..e1 (nldpc_forward.hip).  Every
     # thread of the workgroup copies 16-byte pieces (QMS: 16 messages -> 16 int8 codes).
-    if not S.pipe and SAVECOPY:
+    if not S.pipe:
         for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
             NE = (e1c - e0c) * Z
             w("template <int KIND>")
@@ -1106,13 +784,13 @@ def emit(S: Spec) -> str:
             w("    const int t = threadIdx.x;")
             w("    (void)qp;")
             for g in range(G):
-                src = f"(lds_all + {g * CF * S.nbuf})"
+                src = f"(lds_all + {g * S.cw_floats})"
                 w(f"    if ({g} < nlive) {{")
                 w("        if constexpr (KIND == NLDPC_QMS) {")
                 w(f"            int8_t* dst = (int8_t*)(svb + {(g * S.E + e0c) * Z});")
                 # 16-byte stores only where every absolute address is 16-byte aligned: the saved buffer
                 # is 256-byte aligned, and iteration / block / codeword strides are multiples of E*Z bytes
-                if NE % 16 == 0 and (g * CF * S.nbuf) % 4 == 0 and ((g * S.E + e0c) * Z) % 16 == 0 and (S.E * Z) % 16 == 0:
+                if NE % 16 == 0 and (g * S.cw_floats) % 4 == 0 and ((g * S.E + e0c) * Z) % 16 == 0 and (S.E * Z) % 16 == 0:
                     w(f"            for (int i = t; i < {NE // 16}; i += {S.threads}) {{")
                     w(f"                const float4* s4 = (const float4*)({src} + 16 * i);")
                     w("                uint32_t o[4];")
@@ -1128,7 +806,7 @@ def emit(S: Spec) -> str:
                     w(f"            for (int i = t; i < {NE}; i += {S.threads}) dst[i] = (int8_t)qms_code_p({src}[i], qp);")
                 w("        } else {")
                 w(f"            float* dst = (float*)(svb + {4 * (g * S.E + e0c) * Z});")
-                if NE % 4 == 0 and (g * CF * S.nbuf) % 4 == 0 and ((g * S.E + e0c) * Z) % 4 == 0 and (S.E * Z) % 4 == 0:
+                if NE % 4 == 0 and (g * S.cw_floats) % 4 == 0 and ((g * S.E + e0c) * Z) % 4 == 0 and (S.E * Z) % 4 == 0:
                     w(f"            for (int i = t; i < {NE // 4}; i += {S.threads}) "
                       f"reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>({src})[i];")
                 else:
@@ -1158,37 +836,6 @@ def emit(S: Spec) -> str:
             c += 2
         return phases
 
-    prio = {}
-    if PRIO and S.pipe:
-        # estimated issue cycles per phase and part: VN adds 2, a check-node edge copy ~34 (half-rate
-        # min/select/relu/sign work), an owner LDS message 3 (wrapped copies: compare/select/add)
-        K = len(S.chunks)
-        phases = pipe_phases(K)
-        work = [[0.0] * len(phases) for _ in range(S.P)]
-        for p in range(S.P):
-            vn = sum(len(S.col_edges[j]) * (len(S.col_edges[j]) - 1) // 2 + 2 * len(S.col_edges[j]) + 1
-                     for j in S.reg_cols[p]) * Q
-            work[p][0] += 2 * vn
-            for k, ph in enumerate(phases):
-                for kind_, ci in ph:
-                    e0, e1 = S.chunks[ci][2], S.chunks[ci][3]
-                    if kind_ == "cn":
-                        work[p][k] += 34 * sum(len(S.row_edges[i]) for i, _ in S.cn_units[ci][p])
-                    else:
-                        work[p][k] += 3 * Q * sum(1 for e in S.slots[p] if e0 <= e < e1)
-            if K % 2 == 0:  # the last read-back [R_{K-1}] runs into the next iteration's VN phase
-                work[p][0] += work[p][-1]
-                work[p][-1] = 0
-        for k in range(len(phases)):
-            for par in (0, 1):
-                ps_ = sorted((p for p in range(S.P) if p % 2 == par), key=lambda p: -work[p][k])
-                for r, p in enumerate(ps_):
-                    prio[(p, k)] = max(0, 3 - r)
-
-    def setprio(p, k):
-        if (p, k) in prio:
-            w(f"        __builtin_amdgcn_s_setprio({prio[(p, k)]});")
-
     # this thread's codeword counters (recomputed at each flush: no register held across the iteration)
     cnt_slot = "cntl"  # the kernel passes this codeword's counters
     cnt_flush = "flush_wave" if G == 1 else "flush"  # one codeword per wave: reduce the wave first
@@ -1200,30 +847,21 @@ def emit(S: Spec) -> str:
         w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw, bool dup_, "
-          f"const float* lds_all) {{")
-        if S.pipe and SAVECOPY:
+          f"const float* lds_all, uint32_t* syncc) {{")
+        if S.pipe:
             w("    static_assert(MODE != 1, \"the SAVE kernels use the one-buffer schedule (save_c)\");")
-        for i in range(NP(p)):
-            w(f"    f2 cp{i}[{sp}], xp{i}[{nr}];")
-        for i in range(NS(p)):
+        for i in range(Q):
             w(f"    float cs{i}[{sp}], xs{i}[{nr}];")
         w(f"    float xd[{nd}];")
-        if EVN:
-            for i in range(NS(p)):
-                w(f"    float pe{i}[{nr}];  // EARLYVN: the prefix of the early edges, column by column")
         w("#pragma unroll")
         w(f"    for (int k = 0; k < {sp}; ++k) {{")
-        for i in range(NP(p)):
-            w(f"        cp{i}[k] = f2{{0.f, 0.f}};")
-        for i in range(NS(p)):
+        for i in range(Q):
             w(f"        cs{i}[k] = 0.f;")
         w("    }")
         w("    // this thread's channel values, loaded once for all T iterations")
         for n, j in enumerate(S.reg_cols[p]):
-            for i in range(NP(p)):
-                w(f"    xp{i}[{n}] = f2{{bload(xr, vo, {X(j, 2 * i)}), bload(xr, vo, {X(j, 2 * i + 1)})}};")
-            for i in range(NS(p)):
-                w(f"    xs{i}[{n}] = bload(xr, vo, {X(j, 2 * NP(p) + i)});")
+            for i in range(Q):
+                w(f"    xs{i}[{n}] = bload(xr, vo, {X(j, i)});")
         for n, j in enumerate(S.d1_cols[p]):
             for q in range(Q):
                 w(f"    xd[{n * Q + q}] = bload(xr, vo, {X(j, q)});")
@@ -1244,10 +882,7 @@ def emit(S: Spec) -> str:
         def chan_steps(step_expr, indent):
             w(f"{indent}{{ const cfloat_p wr_ = (cfloat_p)(a.w_vn + (int64_t)({step_expr}) * N);")
             for n, j in enumerate(S.reg_cols[p]):
-                for i in range(NP(p)):
-                    for c in "xy":
-                        w(f"{indent}  xp{i}[{n}].{c} = chan_step<KIND>(xp{i}[{n}].{c}, a, wr_[{j}]);")
-                for i in range(NS(p)):
+                for i in range(Q):
                     w(f"{indent}  xs{i}[{n}] = chan_step<KIND>(xs{i}[{n}], a, wr_[{j}]);")
             for n, j in enumerate(S.d1_cols[p]):
                 for q in range(Q):
@@ -1274,15 +909,13 @@ def emit(S: Spec) -> str:
                   f"__builtin_amdgcn_s_memtime();")
         # UCN: the hard-decision bit array of the codewords starts at zero (bits are OR-ed in); every later
         # iteration's array is cleared in the read-back phase of the iteration before
-        w("    uint32_t d1m = 0;  // UCN: hard decisions of this thread's degree-1 posteriors")
-        w("    uint32_t cdm = 0;  // UCN, D1_BYPASS: hard decisions of the posteriors of this thread's cd entries")
+        w(f"    uint32_t d1m[{nwords(p, 'd1m')}] = {{}};  // UCN: hard decisions of this thread's degree-1 posteriors")
+        w(f"    uint32_t cdm[{nwords(p, 'cdm')}] = {{}};  // UCN, D1_BYPASS: hard decisions of the posteriors of its cd entries")
         w(f"    const rsrc_t apr = make_rsrc(a.app_prev ? a.app_prev + blk * {NZ} : a.xa, a.app_prev ? nlive * {4 * NZ} : 0);")
         w("    if (KIND != NLDPC_NEURAL && a.ucn) {")
         w(f"        for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
         w("        __syncthreads();")
         w("    }")
-        if EVN:  # the all-zero starting state's early sums (the first VN continues them)
-            w(f"    if constexpr (EARLY_VN) vne_p{p}<KIND, MODE>({state_args(p)}{pe_args(p)});")
         w("    for (int it = 0; it < a.T; ++it) {")
         stamp(0)
         w("        if (KIND != NLDPC_NEURAL && a.w_vn) {")
@@ -1302,9 +935,8 @@ def emit(S: Spec) -> str:
         w(f"        const rsrc_t pr = make_rsrc(pp ? pp + blk * {NZ} : a.xa, pp ? nlive * {4 * NZ} : 0);  // no output: stores dropped")
         w("        const uint8_t* pmp = (SAVE && a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t pm = make_rsrc((const float*)(pmp ? pmp + blk * {NZ} : nullptr), pmp ? nlive * {NZ} : 0);")
-        setprio(p, 0)
         if "vn" not in SKIP:
-            w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr{pe_args(p)});")
+            w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
         w(f"        if constexpr (CNT) {{ if (dup_) ps.ec = 0; if (it >= 1) ps.{cnt_flush}({cnt_slot}, it - 1); else ps.ec = 0; }}")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
@@ -1348,7 +980,7 @@ def emit(S: Spec) -> str:
             w("        }")
 
         def buf(ci):
-            return f"lds + {(ci % S.nbuf) * CF}" if S.nbuf > 1 else "lds"
+            return f"lds + {S.region_off[ci]}" if S.region_off[ci] else "lds"
 
         def op_w(ci):
             declare_w(ci)
@@ -1356,10 +988,9 @@ def emit(S: Spec) -> str:
             preload(ci)
             w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, it, sv, vc);")
 
-        def op_cn(ci, loaded=False):
-            if not loaded:
-                w(f"        if constexpr ({WLATE_COND})")
-                preload(ci)
+        def op_cn(ci):
+            w(f"        if constexpr ({WLATE_COND})")
+            preload(ci)
             if "cn" not in SKIP:
                 w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw, xr, apr, cdm);")
 
@@ -1367,7 +998,7 @@ def emit(S: Spec) -> str:
             w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
               f"ps, d1m);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
-                w(f"        if (KIND != NLDPC_NEURAL && !UCNW && {'false' if S.ucn_bw else 'true'} && a.ucn) {{")
+                w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
                 w(f"            for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
                 w("        }")
 
@@ -1377,14 +1008,53 @@ def emit(S: Spec) -> str:
                 op_w(ci)
                 stamp(2 + 3 * ci)
                 w("        __syncthreads();")
-                if SAVECOPY:  # the image holds the chunk's v2c: save it before the check nodes overwrite it
-                    w(f"        if constexpr (SAVE) {{ if (svb) save_c{ci}<KIND>(lds_all, svb, nlive, a.qp); __syncthreads(); }}")
+                # the image holds the chunk's v2c: save it before the check nodes overwrite it
+                w(f"        if constexpr (SAVE) {{ if (svb) save_c{ci}<KIND>(lds_all, svb, nlive, a.qp); __syncthreads(); }}")
                 op_cn(ci)
                 stamp(3 + 3 * ci)
                 w("        __syncthreads();")
                 op_r(ci)
                 stamp(4 + 3 * ci)
                 w("        __syncthreads();")
+        elif S.sched == "split":
+            # Split-barrier schedule over the compacted image (r5): chunk c lives in region c % 2, so W_c overwrites
+            # chunk c-2, whose read-back R_{c-2} runs in the same phase.  Instead of a barrier between them (the
+            # pipe2 schedule's LDS-only [W2, R1] phase), each wave ARRIVES on an LDS counter right after its
+            # read-back and WAITS for all waves' arrivals only just before W_c, after its check rows of chunk c-1:
+            #   [VN, W0] | [CN0, W1] | [R0, arrive, CN1, wait, W2] | ... | [R_{K-2}, arrive, CN_{K-1}] | R_{K-1}, arrive
+            # K + 1 barriers per iteration (pipe2 with K = 4: 6).  Hard barriers stay where a phase reads what
+            # the previous one wrote (CN_c after W_c, R_c after CN_c).  Counter: every wave adds 1 per read-back
+            # round; round it*K + c (R_c of iteration it) is complete when it holds NW * (it*K + c + 1).
+            NW = S.threads // 64
+
+            def arrive():
+                w("        split_arrive(syncc);")
+
+            def wait(done):
+                w(f"        split_wait(syncc, {NW} * ({done}));")
+
+            def bar(k):
+                stamp(2 + k)  # arrival at the barrier that ends phase k (stamp 1: after the VN)
+                w("        __builtin_amdgcn_sched_barrier(0);" if "sync" in SKIP else "        __syncthreads();")
+            if K % 2 == 1:  # region 0's previous chunk is K-1 of the previous iteration, read back just before the VN
+                wait(f"it * {K}")
+            op_w(0)
+            bar(0)
+            for k in range(1, K + 1):
+                if k >= 2:
+                    op_r(k - 2)
+                    arrive()
+                op_cn(k - 1)
+                if k < K:
+                    if k >= 2:
+                        wait(f"it * {K} + {k - 1}")
+                    op_w(k)
+                bar(k)
+            op_r(K - 1)
+            arrive()
+            stamp(3 + K)
+            # UCN: the bits cleared in R_{K-1} must be clear before any wave's next VN sets new ones
+            w("        if (KIND != NLDPC_NEURAL && a.ucn) __syncthreads();")
         else:
             # phases: [W0] | [CN0, W1] | [R0, CN1] | [W2, R1] | [CN2, W3] | [R2, CN3] | ... | [R_{K-1}] (the last
             # read-back runs into the next iteration's VN and W0, whose buffer was last read two phases back).
@@ -1392,23 +1062,8 @@ def emit(S: Spec) -> str:
             phases = pipe_phases(K)
             # phase dependencies hold: each W_c is after R_{c-2}'s phase, each CN_c after W_c's, each R_c after CN_c's
             for k, ph in enumerate(phases):
-                if k > 0 and not (K % 2 == 0 and k == len(phases) - 1):
-                    setprio(p, k)
-                elif k > 0:
-                    setprio(p, 0)  # [R_{K-1}] belongs to the next VN phase
-                early_w = WPHASE and any(kd == "cn" for kd, _ in ph)
-                if early_w:  # WLATE: the phase's check-node weights requested before its other work
-                    for kd, ci in ph:
-                        if kd == "cn":
-                            w(f"        if constexpr ({WLATE_COND})")
-                            preload(ci)
                 for kind_, ci in ph:
-                    if kind_ == "cn":
-                        op_cn(ci, loaded=early_w)
-                    else:
-                        {"w": op_w, "r": op_r}[kind_](ci)
-                    if EVN and kind_ == "r" and ci == 1:  # chunks 0-1 are back: the next VN's early sums
-                        w(f"        if constexpr (EARLY_VN) {{ if (it + 1 < a.T) vne_p{p}<KIND, MODE>({state_args(p)}{pe_args(p)}); }}")
+                    {"w": op_w, "r": op_r, "cn": op_cn}[kind_](ci)
                 stamp(2 + k)  # arrival at the barrier that ends phase k (stamp 1: after the VN)
                 if k < len(phases) - 1:
                     # (timing experiment SKIP=sync: no barrier -- racy results, the cost of waiting at them)
@@ -1418,13 +1073,13 @@ def emit(S: Spec) -> str:
             if K % 2 == 1:
                 w("        __syncthreads();")
             else:  # UCN: the bits cleared in R_{K-1} must be clear before any wave's next VN
-                w(f"        if (KIND != NLDPC_NEURAL && !UCNW && {'false' if S.ucn_bw else 'true'} && a.ucn) __syncthreads();")
+                w("        if (KIND != NLDPC_NEURAL && a.ucn) __syncthreads();")
         w("    }")
         w("    const float* pl = a.outs.p[a.T - 1];")
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
         w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
-        w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr{pe_args(p)});")
+        w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr);")
         w(f"    if constexpr (CNT) {{ if (dup_) ps.ec = 0; ps.{cnt_flush}({cnt_slot}, a.T - 1); }}")
         w("    if (a.c2v_out) {")
         for q in range(Q):
@@ -1435,7 +1090,7 @@ def emit(S: Spec) -> str:
     w("template <int KIND, int MODE>")
     w("__device__ __forceinline__ void kernel_body(const FusedArgs& a) {")
     w("    if (a.sig != kFusedArgsSig) return;  // a launcher built against another FusedArgs layout")
-    w(f"    __shared__ __attribute__((aligned(16))) float lds_all[{CF * S.G_lds * S.nbuf}];")
+    w(f"    __shared__ __attribute__((aligned(16))) float lds_all[{S.cw_floats * S.G_lds}];")
     w("    const int t = threadIdx.x;")
     w(f"    // every wave lies in one part ({S.lanes_pad} threads per part): the part is wave-uniform")
     w(f"    const int p = __builtin_amdgcn_readfirstlane(t / {S.lanes_pad});")
@@ -1456,13 +1111,17 @@ def emit(S: Spec) -> str:
     w(f"    const uint32_t vc = g < nlive && !dup_ ? 4u * (g * {S.E * Z} + u) : 0x80000000u;  // [E][Z] c2v state")
     w(f"    const rsrc_t xr = make_rsrc(a.xa + blk * {NZ}, nlive * {4 * NZ});")
     w(f"    const rsrc_t cr = make_rsrc(a.c2v_out ? a.c2v_out + blk * {S.E * Z} : a.xa, nlive * {4 * S.E * Z});")
-    w(f"    float* lds = lds_all + (dup_ ? {G} : g) * {CF * S.nbuf};  // (repeating lanes: their own region)")
+    w(f"    float* lds = lds_all + (dup_ ? {G} : g) * {S.cw_floats};  // (repeating lanes: their own region)")
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
     w(f"    __shared__ int cnt_all[{G * 32}];  // count-only decode: per codeword, two iterations per word")
     w(f"    __shared__ uint32_t app_all[{S.G_lds * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
+    w("    __shared__ uint32_t syncc[1];  // split schedule: waves' read-back arrivals")
+    if S.sched == "split":
+        w("    if (t == 0) syncc[0] = 0u;")
+        w("    __syncthreads();")
     w(f"    uint32_t* appw = app_all + (dup_ ? {G} : g) * {S.N * S.WZX};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
-    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_, lds_all)",
+    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_, lds_all, syncc)",
               indent="    ")
     w("    if constexpr (CNT) {")
     w("        __syncthreads();")
@@ -1474,7 +1133,6 @@ def emit(S: Spec) -> str:
     w("    kernel_body<KIND, MODE>(a);")
     w("}")
     w("#undef D1_BYPASS")
-    w("#undef UCNW")
     w("#undef ROA")
     w("#undef SAVE")
     w("#undef CNT")
@@ -1629,11 +1287,9 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     w("template <int KIND, int DC, int TIED, int Q0, int Q1>  // the row's copies Q0 .. Q1-1")
     w("__device__ __forceinline__ void cnb_row(float* rp, const char* sq, int u, const FusedBwdArgs& a, int it, "
       "int e0, int row, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
-    # NLDPC_GEN_BWDSB bit 0: a scheduling fence before each row; bit 1: after each lane copy.  Default 2
-    # (per copy only): the row fence pushed the tied QMS kernel to 123 VGPR spills (21 without) and cfg5's
-    # backward measured 27.97 -> 27.32 ms without it (0 = no fence at all: 27.49; profiles/r4_ab.txt)
-    if BWDSB & 1:
-        w("    __builtin_amdgcn_sched_barrier(0);  // one row at a time (register pressure)")
+    # a scheduling fence after each lane copy, none per row: the row fence pushed the tied QMS kernel to 123
+    # VGPR spills (21 without) and cfg5's backward measured 27.97 -> 27.32 ms without it (no fence at all:
+    # 27.49; profiles/r4_ab.txt)
     w("    float wv[DC], bv[DC];")
     w("    const cfloat_p wc = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E + e0) : nullptr;")
     w("    const cfloat_p bs = a.bias ? (cfloat_p)(a.bias + (int64_t)it * E + e0) : nullptr;")
@@ -1651,16 +1307,13 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     w("#pragma unroll")
     w("        for (int k = 0; k < DC; ++k) bv[k] = 0.f;")
     w("    }")
-    if not GWQ:
-        w("    float gwa[DC], gba[DC];")
-        w("#pragma unroll")
-        w("    for (int k = 0; k < DC; ++k) gwa[k] = gba[k] = 0.f;")
     w("#pragma unroll")
     w("    for (int q = Q0; q < Q1; ++q) {")
-    if GWQ:  # per-copy partial sums (slot q of the wave's Q): no accumulator lives across the copies
-        w("        float gwa[DC], gba[DC];")
-        w("#pragma unroll")
-        w("        for (int k = 0; k < DC; ++k) gwa[k] = gba[k] = 0.f;")
+    # per-copy partial sums (slot q of the wave's Q): no accumulator lives across the copies (QMS z=384 with
+    # 3 chunks 3135 -> 16 spilled VGPRs against per-lane accumulators over the copies)
+    w("        float gwa[DC], gba[DC];")
+    w("#pragma unroll")
+    w("        for (int k = 0; k < DC; ++k) gwa[k] = gba[k] = 0.f;")
     w("        auto load_m = [&](int k) {  // saved v2c of edge k at check copy h = u + q*ZT")
     if SBY:
         w("            if constexpr (KIND == NLDPC_QMS)")
@@ -1691,18 +1344,6 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     w("            cn_bwd_ms<DC, KIND>(load_m, rp + q * ZT, Z, wv, bv, KIND == NLDPC_NEURAL || wc, a.qbit, a.lo, a.hi, "
       "gwa, gba);")
     w("        }")
-    def flush(indent):
-        w(f"{indent}if (a.p_cn) {{")
-        w("#pragma unroll")
-        w(f"{indent}    for (int k = 0; k < DC; ++k) {{ const float s_ = wave_sum(dup_ ? 0.f : gwa[k]); "
-          f"if (lane0) a.p_cn[pc + e0 + k] = s_; }}")
-        w(f"{indent}}}")
-        w(f"{indent}if (KIND == NLDPC_NEURAL && a.p_bias) {{")
-        w("#pragma unroll")
-        w(f"{indent}    for (int k = 0; k < DC; ++k) {{ const float s_ = wave_sum(dup_ ? 0.f : gba[k]); "
-          f"if (lane0) a.p_bias[pc + e0 + k] = s_; }}")
-        w(f"{indent}}}")
-
     def flush_q(indent):  # this copy's wave sums, added up over the row's copies by lane 0 in LDS
         for arr, dst, off, cond in (("gwa", "a.p_cn", "0", "a.p_cn"), ("gba", "a.p_bias", "MDC", "KIND == NLDPC_NEURAL && a.p_bias")):
             w(f"{indent}if ({cond}) {{")
@@ -1721,7 +1362,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
             w(f"{indent}}}")
     # tied CN weight (NLDPC_FLAG_CN_TIED): every edge's contribution joins the wave's running sum (one wave
     # reduction per iteration, written by bwd_p into the part's designated edge); the row's entries get 0
-    def tied(indent, last):
+    def tied(indent):
         # (one wave reduction per row copy into the wave's LDS sum: a per-lane running sum across the rows,
         # no reduction inside the row loop, made the register allocator spill 5 520 VGPRs)
         w(f"{indent}if constexpr (TIED) {{")
@@ -1731,17 +1372,11 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w(f"{indent}    const float s_ = wave_sum(dup_ ? 0.f : t_);")
         w(f"{indent}    if (lane0) gacc[0] += s_;")
         w(f"{indent}}} else {{")
-    if GWQ:
-        tied("        ", f"q == {Q - 1}")
-        flush_q("            ")
-        w("        }")
-    if BWDSB & 2:
-        w("        __builtin_amdgcn_sched_barrier(0);  // one check copy at a time: the state owns the registers")
+    tied("        ")
+    flush_q("            ")
+    w("        }")
+    w("        __builtin_amdgcn_sched_barrier(0);  // one check copy at a time: the state owns the registers")
     w("    }")
-    if not GWQ:
-        tied("    ", "true")
-        flush("        ")
-        w("    }")
     w("}")
     for p in range(S.P):
         for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
@@ -1751,8 +1386,8 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
             w("    asm volatile(\"\" : \"+v\"(u));")
             w("    constexpr int SB = saved_msg_bytes<KIND>();")
             # whole rows per part (untied: a row's per-edge sums add up over its copies in the wave's LDS
-            # slots; tied: one wave sum per row copy); NLDPC_GEN_TIEDUNITS=1: the tied kernel by (row, copy)
-            # units balanced over the parts, as the forward's check nodes
+            # slots; tied: one wave sum per row copy; by (row, copy) units as the forward: 28.33 vs 27.87 ms,
+            # profiles/r4c_ab_cfg5.txt)
             rows = sorted(S.cn_rows[ci][p], key=lambda i: -len(S.row_edges[i]))
             w("    if constexpr (!TIED) {")
             for i in rows:
@@ -1761,11 +1396,10 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 w(f"        cnb_row<KIND, {len(es)}, 0, 0, {Q}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, svr, "
                   "vcw, pc, lane0, dup_, gacc);")
             w("    } else {")
-            for i, q in (S.cn_units[ci][p] if TIED_UNITS else [(i, None) for i in rows]):
+            for i in rows:
                 es = S.row_edges[i]
                 off = (es[0] - e0c) * Z
-                q0, q1 = (q, q + 1) if q is not None else (0, Q)
-                w(f"        cnb_row<KIND, {len(es)}, 1, {q0}, {q1}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, "
+                w(f"        cnb_row<KIND, {len(es)}, 1, 0, {Q}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, "
                   "svr, vcw, pc, lane0, dup_, gacc);")
             w("    }")
             w("}")
@@ -1877,7 +1511,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     STF = S.stage_floats
     if SBY:
         w(f"    static_assert(saved_msg_bytes<KIND>() == {SBY}, \"kernel built for another saved-message width\");")
-    GST = 2 * S.max_dc if GWQ and Q > 1 else 1  # per-wave sums (lane 0): a row's copies, or the tied CN sum
+    GST = 2 * S.max_dc if Q > 1 else 1  # per-wave sums (lane 0): a row's copies, or the tied CN sum
     GA = GST * (S.threads // 64)
     assert 4 * (STF * S.G_lds + CF * S.G_lds + GA) <= 160 * 1024, S.tag
     w(f"    // lds_sh: [{STF * S.G_lds + CF * S.G_lds + GA}] floats, staging | images | sums (declared once in bwd_entry)")
@@ -1940,7 +1574,7 @@ def jit_source(hb, Z, kind, mode):
     point -- nldpc_fx (MODE 0-3) or nldpc_fxb (mode 4, the backward).  Returns (source, geometry dict)."""
     hb = np.asarray(hb, dtype=np.int64)
     G, P, Q = auto_geometry(hb, Z)
-    S = Spec("jit", hb, Z, G, P, Q, pipe=PIPE and mode in (0, 2, 3),  # the SAVE kernels keep one buffer
+    S = Spec("jit", hb, Z, G, P, Q, sched=SCHED if mode in (0, 2, 3) else "one",  # the SAVE kernels keep one buffer
              stage=BWD_STAGE[kind] if mode == 4 else 0)  # (backward: staged saved messages)
     L = ["// GENERATED by gen_fused.py jit_source -- do not edit.", "#include <hip/hip_runtime.h>",
          '#include "nldpc_fused.h"', "namespace nldpc {", emit(S) if mode < 4 else emit_bwd(S, BWD_NS[kind]),
@@ -1952,6 +1586,9 @@ def jit_source(hb, Z, kind, mode):
     else:
         L.append(f'extern "C" __global__ {lb} void nldpc_fxb(nldpc::FusedBwdArgs a) {{ '
                  f"nldpc::{BWD_NS[kind]}_jit::bwd_entry<{kind}, 0>(a); }}")
+    # the argument layout this code object was built for: nldpc_graph_attach_kernel compares it with the
+    # library's before accepting the kernel (a skewed build is refused instead of reading garbage)
+    L.append(f'extern "C" __device__ uint32_t nldpc_sig = nldpc::{"kFusedBwdArgsSig" if mode == 4 else "kFusedArgsSig"};')
     return "\n".join(L) + "\n", {"G": G, "threads": S.threads, "waves_per_part": S.lanes_pad // 64,
                                  "P": P, "Q": Q, "padded": S.padded}
 
@@ -1978,7 +1615,7 @@ def main():
         hb = np.loadtxt(os.path.join(res, fname), int, delimiter="\t")
         if G is None:
             G, P, Q = auto_geometry(hb, Z)
-        specs.append((Spec(tag, hb, Z, G, P, Q, pipe=PIPE), Spec(tag, hb, Z, G, P, Q), not only or tag in only))
+        specs.append((Spec(tag, hb, Z, G, P, Q, sched=SCHED), Spec(tag, hb, Z, G, P, Q), not only or tag in only))
     head = ["// GENERATED by gen_fused.py from the base graphs in resources/ -- do not edit.",
             "#include <hip/hip_runtime.h>"]
     head += ['#include "nldpc_fused.h"', "namespace nldpc {"]
@@ -2001,6 +1638,7 @@ def main():
         for save in MODES:
             src = list(head)
             src.append(body_save if save == 1 else body)
+            src.append(f"uint32_t fused_{S.tag}_sig_s{save}() {{ return kFusedArgsSig; }}  // this unit's FusedArgs layout")
             src.append(f"void* fused_{S.tag}_kernel_s{save}(int kind) {{")
             if on:
                 for k in kinds:
@@ -2018,6 +1656,7 @@ def main():
                 if BWD_NS[k] not in done:
                     done.add(BWD_NS[k])
                     src.append(emit_bwd(Spec(S.tag, S.hb, S.Z, S.G, S.P, S.Q, stage=BWD_STAGE[k]), BWD_NS[k]))
+        src.append(f"uint32_t fused_{S.tag}_sig_bwd() {{ return kFusedBwdArgsSig; }}  // this unit's FusedBwdArgs layout")
         src.append(f"void* fused_{S.tag}_bwd(int kind) {{")
         if on and not NOBWD:
             for k in kinds:
@@ -2026,7 +1665,7 @@ def main():
         src.append("    return nullptr;")
         src.append("}")
         src.append(f"void* fused_{S.tag}_bwd_tied(int kind) {{  // a tied CN weight (NLDPC_FLAG_CN_TIED)")
-        if on and TIED_BWD and not NOBWD:
+        if on and not NOBWD:
             for k in kinds:
                 if k != 3:
                     src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&{BWD_NS[k]}_{S.tag}::bwd_kernel<{k}, 1>);")
@@ -2040,6 +1679,9 @@ def main():
             src.append(f"void* fused_{S.tag}_kernel_s{v}(int kind);")
         src.append(f"void* fused_{S.tag}_bwd(int kind);")
         src.append(f"void* fused_{S.tag}_bwd_tied(int kind);")
+        for v in MODES:
+            src.append(f"uint32_t fused_{S.tag}_sig_s{v}();")
+        src.append(f"uint32_t fused_{S.tag}_sig_bwd();")
         src.append(f"static const int32_t basegraph_{S.tag}[{S.M * S.N}] = "
                    f"{{{', '.join(str(int(x)) for x in S.hb.reshape(-1))}}};")
     src.append("const FusedSpec* fused_specs(int* n) {")
@@ -2048,8 +1690,9 @@ def main():
         ks = ", ".join("{" + ", ".join(f"fused_{S.tag}_kernel_s{v}({k})" for k in range(4)) + "}" for v in MODES)
         kb = ", ".join(f"fused_{S.tag}_bwd({k})" for k in range(4))
         kt = ", ".join(f"fused_{S.tag}_bwd_tied({k})" for k in range(4))
+        sg = ", ".join([f"fused_{S.tag}_sig_s{v}()" for v in MODES] + [f"fused_{S.tag}_sig_bwd()"] * 2)
         src.append(f"        {{\"{S.tag}\", {S.M}, {S.N}, {S.Z}, {S.E}, {S.G}, {S.threads}, basegraph_{S.tag}, "
-                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}, {{{kt}}}}},")
+                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}, {{{kt}}}, {{{sg}}}}},")
     src.append("    };")
     src.append(f"    *n = {len(specs)};")
     src.append("    return tab;")

@@ -115,23 +115,6 @@ __device__ __forceinline__ float posterior(float xav, float P, const FusedArgs& 
     return __builtin_amdgcn_fmed3f(fadd(xo, P), a.lo, a.hi);
 }
 
-// Two variable copies at once.  f2 arithmetic is per-lane IEEE fp32 (v_pk_add_f32 on gfx950: two
-// correctly rounded adds), so a pair computes exactly what two scalar copies would.
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-template <int KIND>
-__device__ __forceinline__ f2 posterior2(f2 xav, f2 P, const FusedArgs& a) {
-    if (KIND == NLDPC_NEURAL) return xav + P;
-    return f2{posterior<KIND>(xav.x, P.x, a), posterior<KIND>(xav.y, P.y, a)};
-}
-
-// one saved v2c message (training forward): fp32, or the QMS int8 code (byte offset = float offset / 4)
-template <int KIND>
-__device__ __forceinline__ void save_v2c(rsrc_t r, uint32_t vc, int elem, float v, const QParams& qp) {
-    if constexpr (KIND == NLDPC_QMS) bstore_i8(r, vc >> 2, elem, qms_code_p(v, qp));
-    else bstore(r, vc, 4 * elem, v);
-}
-
 // Boosted posterior and its clamp mask (saved for the backward): in_range of the pre-clamp value
 template <int KIND>
 __device__ __forceinline__ float posterior_m(float xav, float P, const FusedArgs& a, bool& m) {
@@ -151,12 +134,6 @@ __device__ __forceinline__ float d1_v2c(float cd, const FusedArgs& a) {
     return ZADD ? fadd(fadd(0.f, x), 0.f) : x;
 }
 
-template <int KIND>
-__device__ __forceinline__ f2 chan2(f2 x, const FusedArgs& a) {
-    if (KIND == NLDPC_NEURAL) return x;
-    return f2{chan<KIND>(x.x, a), chan<KIND>(x.y, a)};
-}
-
 // UCN hard-decision exchange (Boosted…py:339-374): the owner of variable copy v of column j ORs the bit
 // APP[j][v] >= 0 into the codeword's LDS bit array (word base + v / 32); the check node of copy h reads
 // the bits of its row's variables at (h + s_e) mod Z and takes their parity (odd = unsatisfied).
@@ -164,50 +141,26 @@ __device__ __forceinline__ void app_or(uint32_t* appw, int base, int v, bool bit
     if (bit) atomicOr(appw + base + (v >> 5), 1u << (v & 31));
 }
 
-// The same bits written a wave at a time (geometries whose waves hold 64 consecutive copies u0 + l of
-// one codeword, Z % 32 == 0): one ballot, two words by lane 0, word 0 repeated at word WZ so that a
-// 32-bit window starting anywhere in [0, Z) lies in two consecutive words.  Every word is rewritten each
-// iteration: no atomics and no clearing.
-template <int WZ>
-__device__ __forceinline__ void app_wave(uint32_t* col, int u, bool bit) {
-    const uint64_t m = __builtin_amdgcn_ballot_w64(bit);
-    if ((threadIdx.x & 63) == 0) {
-        const int wi = u >> 5;
-        col[wi] = (uint32_t)m;
-        col[wi + 1] = (uint32_t)(m >> 32);
-        if (wi == 0) col[WZ] = (uint32_t)m;
-    }
+// Split barrier of the "split" chunk schedule (gen_fused.py): a wave ARRIVES once its LDS reads of a chunk's
+// read-back are done (one lane adds 1 to the workgroup's counter), and a wave about to overwrite that region
+// WAITS until every wave of the round has arrived (counter >= target), with independent work (its check rows)
+// in between instead of a workgroup barrier.  The LDS executes one CU's requests in order, and the waiter's
+// writes issue only after its read of the counter returned: no wave's write can overtake another wave's read.
+__device__ __forceinline__ void split_arrive(uint32_t* cnt) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's read-back loads have returned
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// the two words holding bits b .. b+31 (cyclic mod Z) of a column's vector, b in [0, 2Z), and the shift:
-// the window is alignbit(hi, lo, sh)
-__device__ __forceinline__ void app_win_load(const uint32_t* col, uint32_t b, uint32_t Z, uint32_t& lo, uint32_t& hi,
-                                             uint32_t& sh) {
-    b = min(b, b - Z);  // b mod Z (unsigned: b - Z wraps above b when b < Z)
-    lo = col[b >> 5];
-    hi = col[(b >> 5) + 1];
-    sh = b;
-}
-
-// Lanes l of a wave (copies u0 + l, u0 = the wave's first copy) with u0 + l >= T, as a lane mask: all
-// scalar arithmetic on wave-uniform values (the generated code's wrapped copies, gen_fused.py own_lv)
-__device__ __forceinline__ uint64_t wrap_mask(int T, int u0) {
-    const int sh = T - u0;
-    return sh <= 0 ? ~0ull : (sh >= 64 ? 0ull : (~0ull << sh));
+__device__ __forceinline__ void split_wait(const uint32_t* cnt, int target) {
+    while ((int)__builtin_amdgcn_readfirstlane(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+           target)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
 }
 
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
 // scalar loads (a row's edges are consecutive in C order: one s_load_dwordx8/x16 per row).
 typedef const float __attribute__((address_space(4)))* cfloat_p;
 typedef float __attribute__((address_space(3)))* lds_fp;  // LDS pointer (32-bit)
-
-// NLDPC_CMIN: the min / max / median helpers below as plain C (fminf, fabsf, __builtin_amdgcn_fmed3f)
-// for a translation unit compiled with -mno-amdgpu-ieee -fno-honor-nans (the generated kernels: the
-// decoder's values are never NaN), where the compiler needs no canonicalising v_max per operand and folds
-// |x| into the source modifiers itself; the inline-asm forms (IEEE mode) are opaque to its hazard
-// recognizer, which pads them with s_nop, and to its scheduler.
-#ifndef NLDPC_CMIN
-#define NLDPC_CMIN 0
-#endif
 
 // Neural check node of one check copy of a degree-DC row, in place: m[k] (gathered v2c) -> c2v, with
 // the reference's arithmetic (NeuralLDPCDecoder.py:74-91) specialised to what the Neural rule can
@@ -224,13 +177,9 @@ typedef float __attribute__((address_space(3)))* lds_fp;  // LDS pointer (32-bit
 // on gfx950 against a log-depth tournament (pairs, then merges of 3-4 ops): 6 % fewer SIMD cycles per
 // row copy at 4 waves per SIMD (tools/dev/cn_micro.hip) -- the other waves cover the serial chain.
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
-#if NLDPC_CMIN
-    return max(min(a, b), min(max(a, b), c));  // (the compiler forms v_med3_u32)
-#else
     uint32_t d;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
-#endif
 }
 
 template <int DC>
@@ -254,40 +203,24 @@ __device__ __forceinline__ void two_smallest(const uint32_t (&key)[DC], uint32_t
 // asm: written as fminf/fmaxf the compiler materialises every fabsf (v_and_b32) and, in IEEE mode,
 // canonicalises each operand (v_max_f32 x, x) -- three extra VALU per edge.  Plain VALU, no hazards.
 __device__ __forceinline__ float min_aa(float x, float y) {
-#if NLDPC_CMIN
-    return fminf(fabsf(x), fabsf(y));
-#else
     float d;
     asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(d) : "v"(x), "v"(y));
     return d;
-#endif
 }
 __device__ __forceinline__ float max_aa(float x, float y) {
-#if NLDPC_CMIN
-    return fmaxf(fabsf(x), fabsf(y));
-#else
     float d;
     asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(d) : "v"(x), "v"(y));
     return d;
-#endif
 }
 __device__ __forceinline__ float min_a(float a, float x) {  // min(a, |x|), a >= 0
-#if NLDPC_CMIN
-    return fminf(a, fabsf(x));
-#else
     float d;
     asm("v_min_f32_e64 %0, %1, |%2|" : "=v"(d) : "v"(a), "v"(x));
     return d;
-#endif
 }
 __device__ __forceinline__ float med3_a(float a, float b, float x) {  // med3(a, b, |x|)
-#if NLDPC_CMIN
-    return __builtin_amdgcn_fmed3f(a, b, fabsf(x));
-#else
     float d;
     asm("v_med3_f32 %0, %1, %2, |%3|" : "=v"(d) : "v"(a), "v"(b), "v"(x));
     return d;
-#endif
 }
 
 template <int DC>
@@ -314,49 +247,29 @@ __device__ __forceinline__ void two_smallest_abs(const float (&m)[DC], float& mi
 // profiles/r3_valu_rate2*.txt).  CAP: the reference's masked tile entries (10000) take part as one
 // more element, so the minima come out capped (for an even DC that costs one op instead of two clamps).
 __device__ __forceinline__ float min3_aaa(float x, float y, float z) {
-#if NLDPC_CMIN
-    return fminf(fminf(fabsf(x), fabsf(y)), fabsf(z));
-#else
     float d;
     asm("v_min3_f32 %0, |%1|, |%2|, |%3|" : "=v"(d) : "v"(x), "v"(y), "v"(z));
     return d;
-#endif
 }
 __device__ __forceinline__ float med3_aaa(float x, float y, float z) {
-#if NLDPC_CMIN
-    return __builtin_amdgcn_fmed3f(fabsf(x), fabsf(y), fabsf(z));
-#else
     float d;
     asm("v_med3_f32 %0, |%1|, |%2|, |%3|" : "=v"(d) : "v"(x), "v"(y), "v"(z));
     return d;
-#endif
 }
 __device__ __forceinline__ float min3_ra(float a, float x, float y) {  // min3(a, |x|, |y|)
-#if NLDPC_CMIN
-    return fminf(fminf(a, fabsf(x)), fabsf(y));
-#else
     float d;
     asm("v_min3_f32 %0, %1, |%2|, |%3|" : "=v"(d) : "v"(a), "v"(x), "v"(y));
     return d;
-#endif
 }
 __device__ __forceinline__ float med3_ra(float a, float x, float y) {  // med3(a, |x|, |y|)
-#if NLDPC_CMIN
-    return __builtin_amdgcn_fmed3f(a, fabsf(x), fabsf(y));
-#else
     float d;
     asm("v_med3_f32 %0, %1, |%2|, |%3|" : "=v"(d) : "v"(a), "v"(x), "v"(y));
     return d;
-#endif
 }
 __device__ __forceinline__ float min_rr(float a, float b) {  // v_min_f32 without fminf's canonicalising v_max
-#if NLDPC_CMIN
-    return fminf(a, b);
-#else
     float d;
     asm("v_min_f32_e32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
     return d;
-#endif
 }
 template <int DC, bool CAP>
 __device__ __forceinline__ void two_smallest_abs3(const float (&m)[DC], float& min1, float& min2) {
@@ -380,29 +293,19 @@ __device__ __forceinline__ void two_smallest_abs3(const float (&m)[DC], float& m
     min2 = b;
 }
 
-#ifndef NLDPC_CN_KEYS
-// Float-domain form (default): per edge two min-tracking ops, the argmin compare with |m_k| as a
-// modifier, the epilogue and the sign -- no per-edge key and no per-row key decode.  Exact zeros
-// (the reference's "masked" entries: 0 counts as 10000 in the minimum, and is not positive) are rare
-// after iteration 0; a row copy in which any lane of the wave sees one (min1 == 0) takes a
-// wave-uniform branch that maps each 0 to -20000 (magnitude above the 10000 clamp, not positive) and
-// tracks the minimum again.  Bit-identical to the key form below (-DNLDPC_CN_KEYS) and to cn_core.
-#ifndef NLDPC_CN_MIN3
-#define NLDPC_CN_MIN3 1
-#endif
-#ifndef NLDPC_CN_XSIGN
-#define NLDPC_CN_XSIGN 0
-#endif
-#ifndef NLDPC_CN_MAGI
-#define NLDPC_CN_MAGI 0
-#endif
-#ifndef NLDPC_CN_MAGS
-#define NLDPC_CN_MAGS 0
-#endif
+// Float-domain form: per edge two min-tracking ops, the argmin compare with |m_k| as a modifier, the
+// epilogue and the sign -- no per-edge key and no per-row key decode.  Exact zeros (the reference's
+// "masked" entries: 0 counts as 10000 in the minimum, and is not positive) are rare after iteration 0; a
+// row copy in which any lane of the wave sees one (min1 == 0) takes a wave-uniform branch that maps each
+// 0 to -20000 (magnitude above the 10000 clamp, not positive) and tracks the minimum again.  Bit-identical
+// to cn_core (tests compare the fused and streaming paths).  Measured r3/r4 alternatives, all bit-exact and
+// slower on the cfg3 kernel (profiles/r3b_ab.txt, r4_ab.txt): an integer key per edge (4 %), the magnitude
+// select as sat(a + b - |m|) + v_med3_u32 (48.9 -> 51.4 ms) or as min(|m|, mg2) + v_sub_u32 (51.5 ms),
+// signs by bit arithmetic (noise), two row copies with a packed epilogue.
 template <int DC>
 __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
     float min1, min2, mg1, mg2;
-    if constexpr (NLDPC_CN_MIN3 && DC >= 3) {
+    if constexpr (DC >= 3) {
         // the minima capped at 10000 inside the tracking (even DC) or by one min each (odd DC)
         constexpr bool cap = DC % 2 == 0;
         two_smallest_abs3<DC, cap>(m, min1, min2);
@@ -423,59 +326,6 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         mg1 = __builtin_amdgcn_fmed3f(min1, 0.f, 10000.f);  // the masked tile entries (10000) take part
         mg2 = __builtin_amdgcn_fmed3f(min2, 0.f, 10000.f);  // in the min (min1, min2 >= 0: a clamp)
     }
-#if NLDPC_CN_MAGI
-    // the magnitude select without a compare: with a = bits(mg1) <= b = bits(mg2) (non-negative floats
-    // order as integers) and x = bits(|m_k|), t = sat(a + b - x) is b for the edge holding the minimum
-    // (x == bits(min1)) and <= a for every other edge (x >= bits(min2)), so med3(a, b, t) is the
-    // "minimum over the others" -- v_and + v_sub (full rate) + v_med3_u32 instead of v_cmp_eq into an
-    // SGPR pair, the SGPR-read hazard's s_nop and v_cndmask.  (Odd DC, minima capped after tracking:
-    // min1 > 10000 gives a == b; min1 <= 10000 < min2 gives b == 10000 and t == b exactly at x == min1.)
-    // Experiment, off by default: bit-exact, but the cfg3 kernel measured 5 % slower (48.9 -> 51.4 ms,
-    // profiles/r3b_ab.txt) although it issues fewer half-rate instructions.
-    const uint32_t ma_ = __float_as_uint(mg1), mb_ = __float_as_uint(mg2), ms_ = ma_ + mb_;
-    auto magsel = [&](float x) {
-        uint32_t t, r;
-        asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(t) : "v"(ms_), "v"(__float_as_uint(x) & 0x7fffffffu));
-        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(ma_), "v"(mb_), "v"(t));
-        return __uint_as_float(r);
-    };
-#elif NLDPC_CN_MAGS
-    // the magnitude select as t = min(|m_k|, mg2) (|m_k| a source modifier) and one integer subtract:
-    // the edge holding the minimum (|m_k| == min1) gets t = mg1 (mg1 = min(min1, cap) <= mg2), every other
-    // edge has |m_k| >= min2 >= mg2 and gets t = mg2, so bits(mg1) + bits(mg2) - bits(t) is mg2 for the
-    // first and mg1 for the others (non-negative floats order and subtract as integers; ties give
-    // mg1 == mg2).  One half-rate min and a full-rate v_sub_u32 instead of v_cmp_eq into an SGPR pair
-    // (with its s_nop) and v_cndmask.
-    const uint32_t ms_ = __float_as_uint(mg1) + __float_as_uint(mg2);
-    auto magsel = [&](float x) {
-        float t;
-        asm("v_min_f32_e64 %0, |%1|, %2" : "=v"(t) : "v"(x), "v"(mg2));
-        return __uint_as_float(ms_ - __float_as_uint(t));
-    };
-#else
-    auto magsel = [&](float x) { return fabsf(x) == min1 ? mg2 : mg1; };
-#endif
-#if NLDPC_CN_XSIGN
-    // sign by bit arithmetic (m has no zeros here): the output is positive iff the number of positive
-    // OTHER inputs is odd, i.e. its sign bit is sb_k ^ (xor of all sign bits) ^ (DC & 1) -- one v_xor per
-    // edge into the row's sign word and one bit insert per edge, instead of a compare into a lane
-    // mask and a select (both half-rate on gfx950); no lane masks held in SGPRs
-    uint32_t xs = (DC & 1) ? 0x80000000u : 0u;
-#pragma unroll
-    for (int k = 0; k < DC; ++k) xs ^= __float_as_uint(m[k]);
-    asm volatile("" : "+v"(mg1), "+v"(mg2));
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        const float mag = magsel(m[k]);
-        const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
-        // r = max(., 0) is +0 or positive (or -0: a zero's sign is never observed by the decoder's
-        // sums); the sign bit of m_k ^ xs inserted by one v_bfi_b32
-        uint32_t o;
-        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(o) : "v"(0x7fffffffu), "v"(__float_as_uint(r)),
-            "v"(__float_as_uint(m[k]) ^ xs));
-        m[k] = __uint_as_float(o);
-    }
-#else
     bool pos[DC];
     bool par = false;
 #pragma unroll
@@ -486,79 +336,11 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
     asm volatile("" : "+v"(mg1), "+v"(mg2));
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        const float mag = magsel(m[k]);
-        const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
-        m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
-    }
-#endif
-}
-// Two copies of one row (same weights) at once: the minimum tracking per copy as in neural_row, the
-// epilogue's |x|*w and + b as packed fp32 (v_pk_mul_f32 / v_pk_add_f32: per-lane IEEE, the same two
-// roundings as the scalar form).  Experiment (NLDPC_GEN_CNPAIR2).
-template <int DC>
-__device__ __forceinline__ void neural_row2(float (&ma)[DC], float (&mb)[DC], const float (&w)[DC], const float (&b)[DC]) {
-    float a1, a2, b1, b2;
-    two_smallest_abs<DC>(ma, a1, a2);
-    two_smallest_abs<DC>(mb, b1, b2);
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(a1 == 0.f || b1 == 0.f) != 0, 0)) {
-#pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            ma[k] = ma[k] == 0.f ? -20000.f : ma[k];
-            mb[k] = mb[k] == 0.f ? -20000.f : mb[k];
-        }
-        two_smallest_abs<DC>(ma, a1, a2);
-        two_smallest_abs<DC>(mb, b1, b2);
-    }
-    bool pa[DC], pb[DC];
-    bool para = false, parb = false;
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        pa[k] = ma[k] > 0.f;
-        pb[k] = mb[k] > 0.f;
-        para ^= pa[k];
-        parb ^= pb[k];
-    }
-    float ag1 = __builtin_amdgcn_fmed3f(a1, 0.f, 10000.f), ag2 = __builtin_amdgcn_fmed3f(a2, 0.f, 10000.f);
-    float bg1 = __builtin_amdgcn_fmed3f(b1, 0.f, 10000.f), bg2 = __builtin_amdgcn_fmed3f(b2, 0.f, 10000.f);
-    asm volatile("" : "+v"(ag1), "+v"(ag2), "+v"(bg1), "+v"(bg2));
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        const f2 mag = {fabsf(ma[k]) == a1 ? ag2 : ag1, fabsf(mb[k]) == b1 ? bg2 : bg1};
-        const f2 t = mag * f2{w[k], w[k]};
-        const f2 r = t + f2{b[k], b[k]};
-        const float ra = relu_mask(r.x), rb = relu_mask(r.y);
-        ma[k] = (para != pa[k]) ? ra : -ra;
-        mb[k] = (parb != pb[k]) ? rb : -rb;
-    }
-}
-#else
-template <int DC>
-__device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
-    constexpr uint32_t kInit = (0x461C4000u << 1) - 2u;  // key of 10000.f
-    uint32_t key[DC];
-    bool pos[DC];
-    bool par = false;
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        key[k] = (__builtin_bit_cast(uint32_t, m[k]) << 1) - 2u;  // one v_lshl_add_u32
-        pos[k] = m[k] > 0.f;
-        par ^= pos[k];
-    }
-    uint32_t min1, min2;
-    two_smallest<DC>(key, min1, min2);
-    min1 = min(min1, kInit);  // the masked tile entries (10000) take part in the min
-    min2 = min(min2, kInit);
-    float mg1 = __builtin_bit_cast(float, (min1 + 2u) >> 1);
-    float mg2 = __builtin_bit_cast(float, (min2 + 2u) >> 1);
-    asm volatile("" : "+v"(mg1), "+v"(mg2));  // decode once per row, not after every per-edge select
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        const float mag = key[k] == min1 ? mg2 : mg1;
+        const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
         const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
         m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
     }
 }
-#endif
 
 // Backward of the fused decoder (training): one workgroup per G codewords walks the iterations in
 // reverse with dL/dc2v in registers (same ownership as the forward's c2v), reading only the saved
@@ -750,7 +532,7 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
                                             float hi, bool ucn, float uf, const float (&wu)[DC]) {
     if constexpr (DC >= 2) {
         float min1, min2;
-        if constexpr (NLDPC_CN_MIN3 && DC >= 3) two_smallest_abs3<DC, false>(m, min1, min2);
+        if constexpr (DC >= 3) two_smallest_abs3<DC, false>(m, min1, min2);
         else two_smallest_abs<DC>(m, min1, min2);
         bool fast = true;
         if constexpr (KIND == NLDPC_MS)
@@ -834,6 +616,8 @@ struct FusedSpec {
     void* bwd[4];              // backward kernels [nldpc_kind]
     int32_t waves_per_part;    // partial-sum slots per workgroup
     void* bwd_tied[4];         // backward kernels for tied CN / VN weights (MODE 5 in fused_launch), or nullptr
+    uint32_t sig[6];           // the argument layout each MODE's unit was built for (kFusedArgsSig / kFusedBwdArgsSig):
+                               // fused_launch refuses a kernel whose layout differs from the launcher's
 };
 
 const FusedSpec* fused_specs(int* n);

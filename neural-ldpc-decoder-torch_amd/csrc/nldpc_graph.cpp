@@ -253,6 +253,10 @@ FusedLaunch fused_launch(const nldpc_graph* g, int mode, int kind) {
     if (g->fused >= 0) {
         int n = 0;
         const FusedSpec& f = fused_specs(&n)[g->fused];
+        // a generated unit built against another argument layout than this launcher (an experiment build
+        // mixing objects) would return at once and leave its outputs unwritten: no kernel, the caller reports
+        // NLDPC_EUNSUPPORTED for path "fused" or decodes on the streaming kernels
+        if (f.sig[mode] != (mode >= 4 ? kFusedBwdArgsSig : kFusedArgsSig)) return L;
         L.host = mode == 5 ? f.bwd_tied[kind] : mode == 4 ? f.bwd[kind] : f.kernels[mode][kind];
         L.G = f.G;
         L.threads = f.threads;
@@ -285,6 +289,18 @@ extern "C" int nldpc_graph_attach_kernel(nldpc_graph* g, int32_t mode, int32_t k
     hipModule_t mod = nullptr;
     NLDPC_HIP_CHECK(hipModuleLoadData(&mod, code));
     hipFunction_t fn = nullptr;
+    {  // the code object's argument layout (gen_fused.py jit_source: nldpc_sig) must be this library's
+        hipDeviceptr_t sp = nullptr;
+        size_t sb = 0;
+        uint32_t sig = 0;
+        if (hipModuleGetGlobal(&sp, &sb, mod, "nldpc_sig") != hipSuccess || sb != sizeof(sig) ||
+            hipMemcpyDtoH(&sig, sp, sizeof(sig)) != hipSuccess ||
+            sig != (mode == 4 ? kFusedBwdArgsSig : kFusedArgsSig)) {
+            (void)hipModuleUnload(mod);
+            return fail(NLDPC_EUNSUPPORTED, "nldpc_graph_attach_kernel: the code object was built for another "
+                                            "kernel argument layout (regenerate it with this library's gen_fused.py)");
+        }
+    }
     hipError_t e = hipModuleGetFunction(&fn, mod, mode == 4 ? "nldpc_fxb" : "nldpc_fx");
     if (e != hipSuccess) {
         (void)hipModuleUnload(mod);

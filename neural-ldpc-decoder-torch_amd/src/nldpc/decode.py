@@ -8,6 +8,7 @@ NeuralLDPCDecoder / BoostedNeuralLDPCDecoder keep the reference's training seman
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 from dataclasses import dataclass
 
 import torch
@@ -225,6 +226,11 @@ class DecodeFn(torch.autograd.Function):
 
 def decode_autograd(graph, cfg, xa, T, *, w_cn=None, w_ucn=None, bias=None, w_vn=None, c2v=None, app_prev=None):
     """Differentiable decode.  Returns (list of T outputs [B, N*Z], final state [B, E, Z]).  c2v: the
-    incoming message state (None = all-zero); gradients flow into it when it requires grad."""
+    incoming message state (None = all-zero); gradients flow into it when it requires grad.
+    cfg.cn_tied is honoured only for a w_cn whose rows are one repeated value by construction (an expand():
+    stride 0 along the edges, as the drop-in module passes sharing code 3); for any other w_cn the per-edge
+    gradient is computed (a tied backward on per-edge weights returns meaningless entries)."""
+    if cfg.cn_tied and (w_cn is None or w_cn.dim() != 2 or w_cn.stride(1) != 0):
+        cfg = dataclasses.replace(cfg, cn_tied=False)
     res = DecodeFn.apply(graph, cfg, T, app_prev, xa, c2v, w_cn, w_ucn, bias, w_vn)
     return list(res[:T]), res[T]

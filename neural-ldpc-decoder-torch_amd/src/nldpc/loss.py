@@ -17,10 +17,13 @@ class BCEMultiFn(torch.autograd.Function):
     When an output needs a gradient, the forward pass also writes every output's gradient for a unit seed
     (nldpc_bce_loss_grad: the logits are read once for both directions), and backward returns those,
     recomputed on the device only if the seed that arrives is not 1 (nldpc_bce_grad_unless_unit) -- the
-    same values as the separate gradient pass for any seed."""
+    same values as the separate gradient pass for any seed.  Those K gradient tensors (the size of the outputs:
+    8.2 GB at cfg5) are held on ctx from the forward until backward runs or the graph is freed; a loss computed
+    with grad enabled but never backpropagated (logging, validation outside torch.no_grad) pays that write and
+    memory for nothing -- pass fuse_grad=False to bce_multi to keep the two-pass form there."""
 
     @staticmethod
-    def forward(ctx, target, coef, *outputs):
+    def forward(ctx, target, coef, fuse_grad, *outputs):
         L = _lib.lib()
         dev = outputs[0].device
         n = outputs[0].numel()
@@ -34,7 +37,7 @@ class BCEMultiFn(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float32, device=dev)
         px, keep = _lib.ptr_array(xs)
         ctx.grads = None
-        if any(ctx.needs_input_grad[2:]) and hasattr(L, "nldpc_bce_loss_grad"):
+        if fuse_grad and any(ctx.needs_input_grad[3:]) and hasattr(L, "nldpc_bce_loss_grad"):
             grads = [torch.empty_like(x) for x in xs]
             pg, keep_g = _lib.ptr_array(grads)
             st = L.nldpc_bce_loss_grad(px, K, c, _lib.ptr(t), n, _lib.ptr(loss), pg, _lib.ptr(work),
@@ -68,9 +71,10 @@ class BCEMultiFn(torch.autograd.Function):
         st = entry(px, K, c, _lib.ptr(t), n, _lib.ptr(gs), pg, _lib.stream_of(dev))
         del k1, k2
         _lib.check(st, "nldpc_bce_grad")
-        return (None, None, *grads)
+        return (None, None, None, *grads)
 
 
-def bce_multi(outputs, target, coef):
-    """Differentiable multi-term BCE-with-logits on ROCm tensors (see BCEMultiFn)."""
-    return BCEMultiFn.apply(target, list(coef), *outputs)
+def bce_multi(outputs, target, coef, fuse_grad: bool = True):
+    """Differentiable multi-term BCE-with-logits on ROCm tensors (see BCEMultiFn).  fuse_grad=False: the loss
+    pass writes no gradients ahead of a backward (for a loss that is only logged)."""
+    return BCEMultiFn.apply(target, list(coef), bool(fuse_grad), *outputs)

@@ -566,3 +566,27 @@ def test_qms_inactive_quantiser_runs_on_streaming_path(q):
                           w_cn=lambda t: w_cn[t], w_ucn=lambda t: None, w_vn=lambda t: None)
     for t in range(T):
         assert torch.equal(outs[t].cpu(), ref[t]), f"iteration {t}"
+
+
+def test_attach_refuses_a_code_object_of_another_argument_layout(tmp_path):
+    """a kernel built against another FusedArgs layout used to return at once and leave its outputs
+    unwritten with NLDPC_OK.  Run-time code objects carry the layout they were built for (nldpc_sig) and
+    nldpc_graph_attach_kernel refuses a mismatch with NLDPC_EUNSUPPORTED; the library's own kernels are checked
+    the same way in fused_launch (FusedSpec::sig)."""
+    import ctypes
+    import subprocess
+    from nldpc import _lib, jit
+    gen = jit._generator()
+    src, geo = gen.jit_source(BG2, 52, 3, 0)
+    assert "nldpc_sig = nldpc::kFusedArgsSig" in src
+    bad = src.replace("nldpc_sig = nldpc::kFusedArgsSig", "nldpc_sig = 0x12345678u")
+    s, co = str(tmp_path / "k.hip"), str(tmp_path / "k.co")
+    open(s, "w").write(bad)
+    subprocess.run([jit.HIPCC, *jit.FLAGS, "-O1", s, "-o", co], check=True, capture_output=True)
+    data = open(co, "rb").read()
+    g = _graph(BG2, 52)
+    h = g.handle(DEV)
+    st = _lib.lib().nldpc_graph_attach_kernel(h, 0, 3, ctypes.create_string_buffer(data, len(data)), len(data),
+                                               geo["G"], geo["threads"], geo["waves_per_part"])
+    assert st == _lib.NLDPC_EUNSUPPORTED
+    assert "argument layout" in _lib.lib().nldpc_last_error().decode()

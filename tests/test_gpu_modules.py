@@ -310,6 +310,13 @@ def test_bce_loss_grad_one_pass_equals_two_passes(seed_scale):
     assert loss.item() == ref_loss.item()
     for o, r in zip(outs, grads):
         assert torch.equal(o.grad.view(torch.int32), r.view(torch.int32))
+    # the two-pass opt-out (fuse_grad=False) gives the same loss and gradients
+    outs2 = [x.to(DEV).requires_grad_() for x in xs]
+    loss2 = bce_multi(outs2, y, coef, fuse_grad=False)
+    (seed_scale * loss2).backward()
+    assert loss2.item() == ref_loss.item()
+    for o, r in zip(outs2, grads):
+        assert torch.equal(o.grad.view(torch.int32), r.view(torch.int32))
 
 
 @pytest.mark.gpu

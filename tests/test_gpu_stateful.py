@@ -106,3 +106,40 @@ def test_resume_after_caller_refills_input(dtype, nw):
         got = dut(x2, target_iter=list(range(k, T)))
     for t, (a, b) in enumerate(zip(got, ref)):
         assert torch.equal(a, b), f"iteration {k + t}: {(a != b).sum().item()} values differ"
+
+
+@pytest.mark.parametrize("dtype,ucn", [("MS", True), ("QMS", False)])
+def test_dropped_final_state_recomputes_bit_identical(dtype, ucn):
+    """a call that runs up to the last iteration does not write self.llr[T] (keep_state=False, the
+    fused kernel skips 19.8 GB at cfg3); reading it afterwards recomputes it from the call's record.  That
+    state must equal, bit for bit, the state of the same decode run with keep_state=True -- and it is a
+    constant (no graph), unlike the reference's attached tensor (the module docstring says so)."""
+    import dataclasses
+    import boosted_neural_ldpc_decoder as bd
+    from boosted_neural_ldpc_decoder.BoostedNeuralLDPCDecoder import BoostedNeuralLDPCDecoder
+    from boosted_neural_ldpc_decoder.struct.DecoderType import DecoderType
+    from boosted_neural_ldpc_decoder.struct.NodeWeightSharingConfig import NodeWeightSharingConfig as NW
+    from nldpc.decode import decode_autograd
+    T, Z, B = 6, 384, 3
+    conn = bd.ConnectingMatrixTorch(bd.ConnectingMatrix(Z, BG2), device=DEV)
+    model = BoostedNeuralLDPCDecoder(T, B, conn, node_weight_sharing_config=NW(1, 1 if ucn else 0, 2),
+                                     decoding_type=getattr(DecoderType, dtype), decoder_qms_qbit=5).to(DEV)
+    gen = torch.Generator().manual_seed(77)
+    with torch.no_grad():
+        for p in model.parameters():
+            p.copy_(0.6 + 0.8 * torch.rand(p.shape, generator=gen))
+    x = (2 * (-1 + 0.8 * torch.randn(B, 52, Z, generator=gen)) / 0.64).float()
+    if dtype == "QMS":
+        x = torch.clamp(torch.round(2 * x) / 2, -7.5, 7.5)
+    x = x.to(DEV)
+    with torch.no_grad():
+        model(x)
+    assert isinstance(model.llr[T], BoostedNeuralLDPCDecoder._Pending)  # not written by the fused kernel
+    rec = model.llr[T].rec
+    got = model._state(T)
+    assert got is not None and got.shape == (B, int(model.sum_edge), Z) and not got.requires_grad
+    cfg = dataclasses.replace(rec["cfg"], keep_state=True)
+    with torch.no_grad():
+        _, ref = decode_autograd(conn.graph, cfg, x, T, w_cn=rec["w_cn"], w_ucn=rec["w_ucn"], w_vn=rec["w_vn"],
+                                 c2v=None, app_prev=None)
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
