@@ -92,7 +92,10 @@ int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t*
  *      kind, with the geometry they were generated for (codewords per workgroup, threads, waves per
  *      part).  The graph keeps the loaded module until nldpc_graph_destroy.  No-op for a graph the
  *      library already covers.  Replaces nothing in the reference (its dense path has no per-Z code);
- *      it is what makes ConnectingMatrix(Z, basegraph) at any Z (ConnectingMatrix.py:5-53) fast. */
+ *      it is what makes ConnectingMatrix(Z, basegraph) at any Z (ConnectingMatrix.py:5-53) fast.
+ *      The code object's global nldpc_sig (the kernel argument layout it was generated for) must be this
+ *      library's, else NLDPC_EUNSUPPORTED (r5: a skewed build is refused instead of running a kernel that
+ *      leaves its outputs unwritten). */
 int nldpc_graph_attach_kernel(nldpc_graph* g, int32_t mode, int32_t kind, const void* code, size_t bytes,
                               int32_t G, int32_t threads, int32_t waves_per_part);
 /* (ABI 3) *mask: bit (mode * 4 + kind) set when that fused kernel exists for the graph (modes as above) */

@@ -71,9 +71,6 @@ def app_words(N, Z):
 WLATE = os.environ.get("NLDPC_GEN_WLATE", "boosted")
 WLATE_COND = {"boosted": "KIND != NLDPC_NEURAL", "0": "false", "1": "true"}[WLATE]
 NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"  # experiment builds without backward kernels (faster)
-# Decode / count-only chunk schedule (Spec sched): "split" (default, r5) or "pipe2" (r2-r4); experiments:
-# "split<K>" forces K chunks, "split@r1,r2,.." the chunks' first rows
-SCHED = os.environ.get("NLDPC_GEN_SCHED", "split")
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
 # chosen by auto_geometry
@@ -162,19 +159,13 @@ def balance(items, weight, P):
 class Spec:
     def __init__(self, tag, hb, Z, G, P, Q, sched="one", stage=0):
         """sched: the per-iteration chunk schedule -- "one" (one LDS image: write | check nodes | read-back
-        per chunk; the SAVE kernels), "pipe2" (two buffers, r2) or "split" (two buffers over the compacted
-        image, split barriers, r5: the decode and count-only kernels); see emit().
+        per chunk; the SAVE kernels) or "pipe2" (two buffers, pipelined: the decode and count-only kernels);
+        see emit().
         stage (backward kernels): bytes per message of the saved v2c staged in LDS beside the chunk
         image (4 fp32, 1 QMS int8 codes; 0 = none, the check nodes gather from global memory)."""
         assert Z % Q == 0
         self.tag, self.hb, self.Z, self.G, self.P, self.Q = tag, hb, Z, G, P, Q
-        kforce = None
-        if sched.startswith("split@"):  # (a cut list for another graph's rows: the automatic choice)
-            cuts = tuple(int(r) for r in sched[6:].split(","))
-            sched, kforce = "split", (cuts if max(cuts) < hb.shape[0] else None)
-        elif sched.startswith("split") and sched != "split":
-            sched, kforce = "split", int(sched[5:])
-        assert sched in ("one", "pipe2", "split"), sched
+        assert sched in ("one", "pipe2"), sched
         self.sched = sched
         self.pipe = sched != "one"  # two LDS buffers (not the SAVE kernels' schedule)
         self.ZT = Z // Q
@@ -220,16 +211,6 @@ class Spec:
         row_max = max(len(r) for r in self.row_edges)
         if self.pipe:  # two buffers; only the count-only counters (G*128 B) share the remaining KiB
             cap = ((160 * 1024 - 1024 - 4 * GL * app_words(self.N, Z)) // (8 * GL) - (32 if GL > 1 else 0)) // Z
-        # LDS slot of each edge in a chunk image.  "split": the image is compacted to the edges of the
-        # columns of degree > 1 -- every decode kind bypasses LDS for its degree-1 edges (D1_BYPASS), so the
-        # 38 degree-1 slots of BG2 would never be written -- and a chunk's slots are consecutive (C order).
-        d1e = {self.col_edges[j][0] for j in single}
-        self.compact = sched == "split"
-        self.slot = {}
-        for e in range(self.E):
-            if not (self.compact and e in d1e):
-                self.slot[e] = len(self.slot)
-        self.NS = len(self.slot)
 
         def chunking(cap, stage):
             chunks, r0 = [], 0  # (row_begin, row_end, edge_begin, edge_end)
@@ -249,10 +230,7 @@ class Spec:
             sf = -(-(max(e1 - e0 for _, _, e0, e1 in chunks) * Z * stage) // 16) * 4 if stage else 0
             return chunks, cf, sf
 
-        if sched == "split":
-            self._split_chunks(d1e, kforce)
-            got = (self.chunks, None, 0)
-        elif stage:  # the largest chunks whose image and staged messages fit beside each other
+        if stage:  # the largest chunks whose image and staged messages fit beside each other
             c = cap
             while c >= row_max:
                 got = chunking(c, stage)
@@ -263,15 +241,14 @@ class Spec:
                 stage = 0  # a row and its staged messages do not fit: gather from global memory
             if stage:
                 cap = c
-        if sched != "split":
-            got = chunking(cap, stage)
-            if got is None:
-                raise SystemExit(f"{tag}: a single check row does not fit in LDS")
-            self.chunks, self.chunk_floats, self.stage_floats = got
-            self.nbuf = 2 if self.pipe and len(self.chunks) > 1 else 1  # (one chunk: the second buffer would stay unused)
-            # LDS float offset of chunk c's image in a codeword's block, and the block's size
-            self.region_off = [(c % self.nbuf) * self.chunk_floats for c in range(len(self.chunks))]
-            self.cw_floats = self.chunk_floats * self.nbuf
+        got = chunking(cap, stage)
+        if got is None:
+            raise SystemExit(f"{tag}: a single check row does not fit in LDS")
+        self.chunks, self.chunk_floats, self.stage_floats = got
+        self.nbuf = 2 if self.pipe and len(self.chunks) > 1 else 1  # (one chunk: the second buffer would stay unused)
+        # LDS float offset of chunk c's image in a codeword's block, and the block's size
+        self.region_off = [(c % self.nbuf) * self.chunk_floats for c in range(len(self.chunks))]
+        self.cw_floats = self.chunk_floats * self.nbuf
         self.stage = stage
         # LDS-DMA width of the staging: 16 B when every chunk's block (and the per-codeword stride of
         # the saved buffer) is a multiple of 16 B, else 4 B
@@ -290,6 +267,7 @@ class Spec:
         # Register room: a unit's degree-1 edges stay in its part's registers for the whole decode (D1_BYPASS,
         # `cd`), on top of the part's state; a part is offered a unit only while state + cd fits REG_ROOM (the
         # z=384 parts 0/1 hold 69/66 state floats), else the least-loaded part takes it anyway.
+        d1e = {self.col_edges[j][0] for j in single}
         nd1 = [sum(1 for e in self.row_edges[i] if e in d1e) for i in range(self.M)]
         regs = [Q * len(sl) for sl in self.slots]
         self.cn_units = []
@@ -308,52 +286,6 @@ class Spec:
         self.max_dc = max(len(r) for r in self.row_edges)
         self.hb_cols = cols  # column of each C-order edge
 
-    def _split_chunks(self, d1e, kforce):
-        """The "split" schedule's chunks: K contiguous row ranges over the compacted image, chunk c in region c % 2
-        (region A for even chunks, B for odd ones: A + B slots fit LDS beside the UCN bits and counters).  An
-        iteration has K + 1 barriers (emit()), so the fewest chunks that fit win; among those, the split whose
-        busiest check-node phase (check rows of chunk k-1 plus the owner traffic of chunks k and k-2) is lightest."""
-        Z, Q, GL = self.Z, self.Q, self.G_lds
-        cap = ((160 * 1024 - 1024 - 4 * GL * app_words(self.N, Z)) // (4 * GL) - (32 if GL > 1 else 0)) // Z
-        nsl = [sum(1 for e in self.row_edges[i] if e not in d1e) for i in range(self.M)]  # LDS slots per row
-        cnw = [len(self.row_edges[i]) + 1 for i in range(self.M)]  # check-node work per row copy
-        pre_s, pre_w = np.concatenate([[0], np.cumsum(nsl)]), np.concatenate([[0], np.cumsum(cnw)])
-        if max(nsl) > cap:
-            raise SystemExit(f"{self.tag}: a single check row does not fit in LDS")
-        import itertools
-        best = None
-        for K in ([len(kforce) + 1] if isinstance(kforce, tuple) else [kforce] if kforce else range(1, self.M + 1)):
-            for cut in ([kforce] if isinstance(kforce, tuple) else itertools.combinations(range(1, self.M), K - 1)):
-                b = (0,) + cut + (self.M,)
-                sl = [int(pre_s[b[c + 1]] - pre_s[b[c]]) for c in range(K)]
-                A = max(sl[0::2])
-                B = max(sl[1::2]) if K > 1 else 0
-                if A + B > cap or min(sl) == 0 and K > 1:
-                    continue
-                cn = [int(pre_w[b[c + 1]] - pre_w[b[c]]) for c in range(K)]
-                own = lambda c: sl[c] if 0 <= c < K else 0  # noqa: E731
-                load = [cn[k - 1] + 0.25 * (own(k) + own(k - 2)) for k in range(1, K + 1)]
-                key = (max(load), sum(x * x for x in load))
-                if best is None or key < best[0]:
-                    best = (key, b, A, B)
-            if best is not None:
-                break
-        if best is None:
-            raise SystemExit(f"{self.tag}: no split chunking fits LDS")
-        _, b, A, B = best
-        self.chunks = []
-        for c in range(len(b) - 1):
-            s0 = int(pre_s[b[c]])
-            self.chunks.append((b[c], b[c + 1], s0, int(pre_s[b[c + 1]])))
-        self.region_slots = (A, B)
-        self.region_off = [0 if c % 2 == 0 else A * Z for c in range(len(self.chunks))]
-        cw = (A + B) * Z
-        if GL > 1:  # codeword stride = 1 (mod 32 banks) so lanes of different codewords do not collide
-            cw += (1 - cw) % 32
-        self.cw_floats = cw
-        self.chunk_floats = max(A, B) * Z
-        self.nbuf = 2 if len(self.chunks) > 1 else 1
-
 
 def emit(S: Spec) -> str:
     Z, G, Q, ZT, NZ = S.Z, S.G, S.Q, S.ZT, S.N * S.Z
@@ -363,9 +295,7 @@ def emit(S: Spec) -> str:
     # wrapped lane copies by scalar lane masks (own_lv): needs waves of 64 consecutive copies of one codeword
     w(f"// ---- {S.tag}: M={S.M} N={S.N} E={S.E} Z={Z}; workgroup = {G} codeword(s) x {S.P} part(s) x {ZT} lanes "
       f"= {S.threads} threads{' (padded parts)' if S.padded else ''}, {Q} cop{'y' if Q == 1 else 'ies'} per lane; register slots/part "
-      f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B; schedule {S.sched}"
-      + (f", regions {S.region_slots} slots, chunks {[(c[0], c[1], c[3] - c[2]) for c in S.chunks]} (rows, slots)"
-         if S.sched == "split" else ""))
+      f"{[len(s) * Q for s in S.slots]}; {len(S.chunks)} LDS chunk(s) of <= {CF * G * 4} B")
     w(f"namespace fused_{S.tag} {{")
     w(f"constexpr int Z = {Z}, ZT = {ZT}, N = {S.N}, E = {S.E};")
     w("// degree-1 edges bypass LDS (Neural inference; see the check-node section)")
@@ -551,7 +481,7 @@ def emit(S: Spec) -> str:
         check copy h = (v - s_e) mod Z of the chunk's check-ordered image.  Only one of the Q copies
         of a shifted edge can wrap inside the lane range; the others are a constant offset."""
         cq = (q * ZT - int(S.shift[e])) % Z
-        base = (S.slot[e] - e0) * Z + cq
+        base = (e - e0) * Z + cq
         if cq + ZT <= Z:
             return f"{base} + u"
         return f"{base} + u - (u >= {Z - cq} ? {Z} : 0)"
@@ -561,9 +491,8 @@ def emit(S: Spec) -> str:
 
     for p in range(S.P):
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
-            mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= S.slot[e] < e1]
-            # (compacted image: the degree-1 edges have no slot -- D1_BYPASS holds for every kind there)
-            d1 = [] if S.compact else [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
+            mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
+            d1 = [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void wr_p{p}_c{ci}({state_params(p, True)}, {x_params(p)}, float* lds, "
               f"int u, const FusedArgs& a, int it, rsrc_t sv, uint32_t vc) {{")
@@ -660,11 +589,9 @@ def emit(S: Spec) -> str:
                 wo += len(S.row_edges[i])
 
             def row_slots(i):
-                """The row's first LDS slot and each slotted edge's float offset from it (compacted image: the
-                row's slots are consecutive, its degree-1 edges have none)."""
+                """The row's first edge and each edge's float offset from it in the chunk image."""
                 es = S.row_edges[i]
-                rb = min((S.slot[e] for e in es if e in S.slot), default=e0c)
-                return rb, {e: (S.slot[e] - rb) * Z for e in es if e in S.slot}
+                return es[0], {e: k * Z for k, e in enumerate(es)}
 
             def rc_load(n):
                 i, q = rcs[n]
@@ -686,11 +613,8 @@ def emit(S: Spec) -> str:
                 w("    }")
                 for k, e in enumerate(es):
                     if e in d1set:
-                        if S.compact:
-                            w(f"    m{n}[{k}] = d1_v2c<KIND, 1>(cd[{S.cd_index[p].index((e, q))}], a);")
-                        else:
-                            w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = d1_v2c<KIND, 1>(cd[{S.cd_index[p].index((e, q))}], a); "
-                              f"else m{n}[{k}] = rq{n}[{off[e]}];")
+                        w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = d1_v2c<KIND, 1>(cd[{S.cd_index[p].index((e, q))}], a); "
+                          f"else m{n}[{k}] = rq{n}[{off[e]}];")
                     elif "cnread" in SKIP:  # (timing experiment: no check-node LDS reads, junk inputs)
                         w(f"    m{n}[{k}] = __uint_as_float(0x3f800000u + ((uint32_t)u << 8) + {k * 977 + n * 131}u);")
                     else:
@@ -754,7 +678,7 @@ def emit(S: Spec) -> str:
                         else:
                             w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, y_, ps);")
                         w(f"            if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m{n}[{k}]);")
-                        w("        }" if S.compact else f"        }} else {{ rq{n}[{off[e]}] = m{n}[{k}]; }}")
+                        w(f"        }} else {{ rq{n}[{off[e]}] = m{n}[{k}]; }}")
                     elif "cnwrite" in SKIP:  # (timing experiment: keep the value live without the LDS write)
                         w(f"        asm volatile(\"\" :: \"v\"(m{n}[{k}]));")
                     else:
@@ -847,7 +771,7 @@ def emit(S: Spec) -> str:
         w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw, bool dup_, "
-          f"const float* lds_all, uint32_t* syncc) {{")
+          f"const float* lds_all) {{")
         if S.pipe:
             w("    static_assert(MODE != 1, \"the SAVE kernels use the one-buffer schedule (save_c)\");")
         for i in range(Q):
@@ -1016,45 +940,6 @@ def emit(S: Spec) -> str:
                 op_r(ci)
                 stamp(4 + 3 * ci)
                 w("        __syncthreads();")
-        elif S.sched == "split":
-            # Split-barrier schedule over the compacted image (r5): chunk c lives in region c % 2, so W_c overwrites
-            # chunk c-2, whose read-back R_{c-2} runs in the same phase.  Instead of a barrier between them (the
-            # pipe2 schedule's LDS-only [W2, R1] phase), each wave ARRIVES on an LDS counter right after its
-            # read-back and WAITS for all waves' arrivals only just before W_c, after its check rows of chunk c-1:
-            #   [VN, W0] | [CN0, W1] | [R0, arrive, CN1, wait, W2] | ... | [R_{K-2}, arrive, CN_{K-1}] | R_{K-1}, arrive
-            # K + 1 barriers per iteration (pipe2 with K = 4: 6).  Hard barriers stay where a phase reads what
-            # the previous one wrote (CN_c after W_c, R_c after CN_c).  Counter: every wave adds 1 per read-back
-            # round; round it*K + c (R_c of iteration it) is complete when it holds NW * (it*K + c + 1).
-            NW = S.threads // 64
-
-            def arrive():
-                w("        split_arrive(syncc);")
-
-            def wait(done):
-                w(f"        split_wait(syncc, {NW} * ({done}));")
-
-            def bar(k):
-                stamp(2 + k)  # arrival at the barrier that ends phase k (stamp 1: after the VN)
-                w("        __builtin_amdgcn_sched_barrier(0);" if "sync" in SKIP else "        __syncthreads();")
-            if K % 2 == 1:  # region 0's previous chunk is K-1 of the previous iteration, read back just before the VN
-                wait(f"it * {K}")
-            op_w(0)
-            bar(0)
-            for k in range(1, K + 1):
-                if k >= 2:
-                    op_r(k - 2)
-                    arrive()
-                op_cn(k - 1)
-                if k < K:
-                    if k >= 2:
-                        wait(f"it * {K} + {k - 1}")
-                    op_w(k)
-                bar(k)
-            op_r(K - 1)
-            arrive()
-            stamp(3 + K)
-            # UCN: the bits cleared in R_{K-1} must be clear before any wave's next VN sets new ones
-            w("        if (KIND != NLDPC_NEURAL && a.ucn) __syncthreads();")
         else:
             # phases: [W0] | [CN0, W1] | [R0, CN1] | [W2, R1] | [CN2, W3] | [R2, CN3] | ... | [R_{K-1}] (the last
             # read-back runs into the next iteration's VN and W0, whose buffer was last read two phases back).
@@ -1115,13 +1000,9 @@ def emit(S: Spec) -> str:
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
     w(f"    __shared__ int cnt_all[{G * 32}];  // count-only decode: per codeword, two iterations per word")
     w(f"    __shared__ uint32_t app_all[{S.G_lds * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
-    w("    __shared__ uint32_t syncc[1];  // split schedule: waves' read-back arrivals")
-    if S.sched == "split":
-        w("    if (t == 0) syncc[0] = 0u;")
-        w("    __syncthreads();")
     w(f"    uint32_t* appw = app_all + (dup_ ? {G} : g) * {S.N * S.WZX};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
-    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_, lds_all, syncc)",
+    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_, lds_all)",
               indent="    ")
     w("    if constexpr (CNT) {")
     w("        __syncthreads();")
@@ -1574,7 +1455,7 @@ def jit_source(hb, Z, kind, mode):
     point -- nldpc_fx (MODE 0-3) or nldpc_fxb (mode 4, the backward).  Returns (source, geometry dict)."""
     hb = np.asarray(hb, dtype=np.int64)
     G, P, Q = auto_geometry(hb, Z)
-    S = Spec("jit", hb, Z, G, P, Q, sched=SCHED if mode in (0, 2, 3) else "one",  # the SAVE kernels keep one buffer
+    S = Spec("jit", hb, Z, G, P, Q, sched="pipe2" if mode in (0, 2, 3) else "one",  # the SAVE kernels keep one buffer
              stage=BWD_STAGE[kind] if mode == 4 else 0)  # (backward: staged saved messages)
     L = ["// GENERATED by gen_fused.py jit_source -- do not edit.", "#include <hip/hip_runtime.h>",
          '#include "nldpc_fused.h"', "namespace nldpc {", emit(S) if mode < 4 else emit_bwd(S, BWD_NS[kind]),
@@ -1615,7 +1496,7 @@ def main():
         hb = np.loadtxt(os.path.join(res, fname), int, delimiter="\t")
         if G is None:
             G, P, Q = auto_geometry(hb, Z)
-        specs.append((Spec(tag, hb, Z, G, P, Q, sched=SCHED), Spec(tag, hb, Z, G, P, Q), not only or tag in only))
+        specs.append((Spec(tag, hb, Z, G, P, Q, sched="pipe2"), Spec(tag, hb, Z, G, P, Q), not only or tag in only))
     head = ["// GENERATED by gen_fused.py from the base graphs in resources/ -- do not edit.",
             "#include <hip/hip_runtime.h>"]
     head += ['#include "nldpc_fused.h"', "namespace nldpc {"]

@@ -141,22 +141,6 @@ __device__ __forceinline__ void app_or(uint32_t* appw, int base, int v, bool bit
     if (bit) atomicOr(appw + base + (v >> 5), 1u << (v & 31));
 }
 
-// Split barrier of the "split" chunk schedule (gen_fused.py): a wave ARRIVES once its LDS reads of a chunk's
-// read-back are done (one lane adds 1 to the workgroup's counter), and a wave about to overwrite that region
-// WAITS until every wave of the round has arrived (counter >= target), with independent work (its check rows)
-// in between instead of a workgroup barrier.  The LDS executes one CU's requests in order, and the waiter's
-// writes issue only after its read of the counter returned: no wave's write can overtake another wave's read.
-__device__ __forceinline__ void split_arrive(uint32_t* cnt) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's read-back loads have returned
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void split_wait(const uint32_t* cnt, int target) {
-    while ((int)__builtin_amdgcn_readfirstlane(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
-           target)
-        __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
-}
-
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
 // scalar loads (a row's edges are consecutive in C order: one s_load_dwordx8/x16 per row).
 typedef const float __attribute__((address_space(4)))* cfloat_p;

@@ -57,6 +57,5 @@ def test_no_pruned_knob_is_read():
     src = open(os.path.join(CS, "gen_fused.py")).read()
     knobs = set(re.findall(r'environ\.get\("(NLDPC_[A-Z_0-9]+)"', src))
     assert knobs <= {"NLDPC_GEN_PARTS", "NLDPC_GEN_SKIP", "NLDPC_GEN_STAMPS", "NLDPC_GEN_GEOM", "NLDPC_GEN_WLATE",
-                     "NLDPC_GEN_NOBWD", "NLDPC_GEN_ONLY", "NLDPC_GEN_KINDS", "NLDPC_FUSED_EXTRA",
-                     "NLDPC_GEN_SCHED"}, knobs
+                     "NLDPC_GEN_NOBWD", "NLDPC_GEN_ONLY", "NLDPC_GEN_KINDS", "NLDPC_FUSED_EXTRA"}, knobs
     assert len(knobs) <= 15

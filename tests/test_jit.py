@@ -24,7 +24,7 @@ def test_every_nr_lifting_size_has_a_geometry():
     assert len(NR_Z) == 51
     for Z in NR_Z:
         G, P, Q = gen.auto_geometry(BG2, Z)
-        S = gen.Spec("t", BG2, Z, G, P, Q, sched="split")
+        S = gen.Spec("t", BG2, Z, G, P, Q, sched="pipe2")
         assert S.threads <= 1024 and S.lanes_pad % 64 == 0 and (S.lanes_pad - S.lanes) * 4 <= S.lanes_pad, Z
         assert max(len(s) for s in S.slots) * Q <= gen.MAX_STATE_REGS, Z
 

@@ -115,7 +115,26 @@ def main(paths):
           f"per cfg3 launch at {CLK_GHZ} GHz ({ITERS_PER_CU:.0f} codeword-iterations per CU)")
     print(f"the north-star 22.9 ms (0.60 of HBM) allows {22.9e-3 * CLK_GHZ * 1e9 / ITERS_PER_CU:.0f} cycles per "
           f"codeword-iteration")
+    return worst
+
+
+def write_json(path, worst, source):
+    """The budget bench.py reads (roofline.issue_floor_ms): busier-set SIMD issue cycles per workgroup-iteration."""
+    import json
+    import os
+    d = json.load(open(path)) if os.path.exists(path) else {}
+    d["fused_bg2_z384::kernel<3, 0>"] = {"simd_issue_cycles_per_wg_iter": int(round(worst)), "G": 1,
+                                          "clock_ghz": CLK_GHZ, "source": source}
+    with open(path, "w") as f:
+        json.dump(d, f, indent=1)
+        f.write("\n")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    args = sys.argv[1:]
+    js = None
+    if args and args[0].startswith("--json="):
+        js, args = args[0][7:], args[1:]
+    worst = main(args)
+    if js:
+        write_json(js, worst, "tools/isa_budget.sh (gfx950 asm of single-part builds of the library's generator)")

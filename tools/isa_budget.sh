@@ -15,4 +15,4 @@ for p in 0 1 2 3 4 5 6 7; do
     -o "$OUT/parts/p$p.s" &
 done
 wait
-python3 "$ROOT/tools/isa_budget.py" "$OUT"/parts/p{0,1,2,3,4,5,6,7}.s
+python3 "$ROOT/tools/isa_budget.py" ${ISA_JSON:+--json=$ISA_JSON} "$OUT"/parts/p{0,1,2,3,4,5,6,7}.s
