@@ -217,6 +217,14 @@ def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings,
                                     "PMC effective clock: the launch time with no stall at all"}
         if r["issue_frac"] > r["frac"]:
             r["bound"] = "valu"
+    # neither ceiling near: the waves mostly wait (PMC SQ_WAIT_ANY over wave-cycles) -- a latency-bound kernel
+    # (the cfg5 backward: LDS round trips and barriers)
+    valu_frac = r.get("valu_issue", {}).get("weighted_frac_of_simd_cycles") or r.get("valu_issue", {}).get("frac_of_peak")
+    wait = pmc.get("wait_any_over_wave_cycles") if pmc else None
+    if r["bound"] == "hbm" and wait is not None and wait >= 0.5 and r["frac"] < 0.5 and (valu_frac or 0) < 0.5:
+        r["bound"] = "latency"
+        r["bound_evidence"] = (f"HBM {r['frac']:.2f} of peak, VALU issue {valu_frac or 0:.2f} of peak, "
+                               f"SQ_WAIT_ANY / wave-cycles {wait:.2f} (PMC)")
     if dom == "fused" and d5_bytes_per_cw:
         # SURVEY §8(d) D5 models a flooding decoder whose E*Z message state crosses HBM every iteration;
         # the fused kernel keeps that state on chip, so this is an equivalent rate, not traffic

@@ -42,10 +42,20 @@ def vclass(op):
 
 def parse(path):
     raw = open(path).read().split("\n")
-    # the loop header: the label the asm comments as "Inner Loop Header"
-    hi = next(i for i, ln in enumerate(raw) if "Loop Header" in ln and ln.startswith(".LBB"))
-    label = raw[hi].split(":")[0]
-    back = next(i for i in range(len(raw) - 1, hi, -1) if raw[i].strip() == f"s_branch {label}")
+    # the iteration loop: of the labels the asm comments as "Loop Header", the one whose body (header to the
+    # last branch back to it) holds the most s_barrier instructions (the Boosted kernels have other loops)
+    best = None
+    for i, ln in enumerate(raw):
+        if "Loop Header" in ln and ln.startswith(".LBB"):
+            label = ln.split(":")[0]
+            ends = [k for k in range(len(raw) - 1, i, -1)
+                    if raw[k].strip().startswith("s_") and raw[k].strip().split()[-1] == label
+                    and "branch" in raw[k]]
+            if ends:
+                nb = sum(1 for k in range(i, ends[0]) if raw[k].strip() == "s_barrier")
+                if best is None or nb > best[0]:
+                    best = (nb, i, ends[0])
+    _, hi, back = best
     phases, cur = [], collections.Counter()
     for ln in raw[hi + 1:back + 1]:
         t = ln.split(";")[0].strip()

@@ -8,7 +8,7 @@ CS=$ROOT/neural-ldpc-decoder-torch_amd/csrc
 OUT=${1:-/tmp/isa}
 mkdir -p "$OUT/parts"
 for p in 0 1 2 3 4 5 6 7; do
-  NLDPC_GEN_PARTS=$p NLDPC_GEN_KINDS=3 NLDPC_GEN_ONLY=bg2_z384 NLDPC_GEN_NOBWD=1 \
+  NLDPC_GEN_PARTS=$p NLDPC_GEN_KINDS=${KIND:-3} NLDPC_GEN_ONLY=bg2_z384 NLDPC_GEN_NOBWD=1 \
     python3 "$CS/gen_fused.py" "$OUT/parts/g$p" "$ROOT/resources" > /dev/null
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
     -I"$ROOT/include" -I"$CS" -x hip --cuda-device-only -S "$OUT/parts/g$p/fused_bg2_z384_s0.hip" \
