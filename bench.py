@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event per-kernel timing")
     ap.add_argument("--no-sweep", action="store_true", help="skip the Eb/N0 1..4 dB BER sweep")
     ap.add_argument("--no-count-only", action="store_true", help="skip the count-only decode timing (F2)")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="decode steps as replays of one captured HIP graph (auto: cfg2, whose 0.1 ms kernel is "
+                         "comparable to the host path of a module call)")
     ap.add_argument("--nw", default="1,1,2", help="cfg3ucn: NodeWeightSharingConfig (cn, ucn, vn) codes")
     ap.add_argument("--kind", default="MS", choices=("MS", "QMS", "SP"), help="cfg3ucn: Boosted decoding type")
     return ap.parse_args()
@@ -367,8 +370,28 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
         state["outs"] = None
         state["outs"] = model(xa)
 
+    use_graph = args.graph == "on" or (args.graph == "auto" and args.workload == "cfg2")
+    graph_info = None
     with torch.no_grad():
         elapsed, prof, step_ms = timed(args, local, dev, step, Prof(not args.no_profile, args.steps * (2 * T + 2)))
+        if use_graph:
+            # the same module call captured once into a HIP graph (stream capture of the library's launch on
+            # torch's stream; outputs in the graph's pool), each step one replay: the host path of a module
+            # call (Python, argument checks, ctypes) leaves the timed loop.  The eager timing above gives the
+            # per-kernel HIP-event profile (events cannot be recorded inside the graph) and is reported beside.
+            eager = {"ms_per_step": round(1000.0 * nd_dist.max_time(elapsed, device=dev) / args.steps, 3),
+                     "ms_per_step_median": round(statistics.median(step_ms), 3)}
+            g = torch.cuda.CUDAGraph()
+            state["outs"] = None
+            with torch.cuda.graph(g):
+                g_outs = model(xa)
+
+            def gstep():
+                g.replay()
+                state["outs"] = g_outs
+
+            elapsed, _, step_ms = timed(args, local, dev, gstep, Prof(False, 0))
+            graph_info = {"replay": True, "eager": eager}
         counts = ber_counts(state["outs"])  # BER / FER per iteration, decoder convention bit = LLR > 0
         # the reference helper itself on the same outputs (literal rule bit = LLR < 0: ~1 - BER)
         from boosted_neural_ldpc_decoder.Functions import Functions
@@ -440,6 +463,8 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
     }
     if count_only is not None:
         res["count_only"] = count_only
+    if graph_info is not None:
+        res["config"]["graph"] = graph_info
     if sweep is not None:
         sweep["ber"] = [b / bits_total for b in sweep["bit_errors"]]
         sweep["fer"] = [f / (world * B) for f in sweep["frame_errors"]]

@@ -71,6 +71,9 @@ def app_words(N, Z):
 WLATE = os.environ.get("NLDPC_GEN_WLATE", "boosted")
 WLATE_COND = {"boosted": "KIND != NLDPC_NEURAL", "0": "false", "1": "true"}[WLATE]
 NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"  # experiment builds without backward kernels (faster)
+# SAVE kernels of one-codeword geometries: lane offsets re-derived per phase, buffer-descriptor saves (r5: the
+# cfg5 training forward 11.57 -> 11.38 ms, profiles/r5i_ab_uremat.txt); NLDPC_GEN_UREMAT=0 turns it off
+UREMAT = os.environ.get("NLDPC_GEN_UREMAT", "1") == "1"
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
 # chosen by auto_geometry
@@ -284,6 +287,8 @@ class Spec:
                 regs[k] += nd1[i]
             self.cn_units.append([sorted(b, key=lambda iq: (-len(self.row_edges[iq[0]]), iq[0], iq[1])) for b in bins])
         self.max_dc = max(len(r) for r in self.row_edges)
+        # UREMAT applies where a wave's lanes are consecutive copies of one codeword: u = (wave base) + lane
+        self.uremat = UREMAT and not self.pipe and G == 1 and not self.padded and self.ZT % 64 == 0  # (the SAVE kernels)
         self.hb_cols = cols  # column of each C-order edge
 
 
@@ -700,7 +705,38 @@ def emit(S: Spec) -> str:
     # The image of chunk c is [G][CF] floats in check order: edge e0+i's message for check copy h at
     # i*Z + h, the saved buffer's layout for this codeword's edges e0..e1 (nldpc_forward.hip).  Every
     # thread of the workgroup copies 16-byte pieces (QMS: 16 messages -> 16 int8 codes).
-    if not S.pipe:
+    if not S.pipe and S.uremat:
+        # (UREMAT: the thread index re-derived by the caller, stores through a buffer descriptor with 32-bit
+        # offsets instead of 64-bit flat addresses -- one codeword per workgroup, 16-byte aligned chunks)
+        for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
+            NE = (e1c - e0c) * Z
+            assert NE % 16 == 0 and (e0c * Z) % 16 == 0 and (S.E * Z) % 16 == 0 and G == 1
+            w("template <int KIND>")
+            w(f"__device__ __forceinline__ void save_c{ci}(const float* lds_all, char* svb, int nlive, const QParams& qp, int t) {{")
+            w("    (void)qp; (void)nlive;")
+            w("    typedef uint32_t v4u __attribute__((ext_vector_type(4)));")
+            w(f"    const rsrc_t sr = make_rsrc((const float*)svb, {S.E * Z} * saved_msg_bytes<KIND>());  // this codeword's saved block")
+            w("    if constexpr (KIND == NLDPC_QMS) {")
+            w(f"        for (int i = t; i < {NE // 16}; i += {S.threads}) {{")
+            w("            const float4* s4 = (const float4*)(lds_all + 16 * i);")
+            w("            uint32_t o[4];")
+            w("#pragma unroll")
+            w("            for (int k = 0; k < 4; ++k) {")
+            w("                const float4 v = s4[k];")
+            w("                o[k] = ((uint32_t)qms_code_p(v.x, qp) & 255u) | (((uint32_t)qms_code_p(v.y, qp) & 255u) << 8) |")
+            w("                       (((uint32_t)qms_code_p(v.z, qp) & 255u) << 16) | ((uint32_t)qms_code_p(v.w, qp) << 24);")
+            w("            }")
+            w(f"            __builtin_amdgcn_raw_buffer_store_b128(v4u{{o[0], o[1], o[2], o[3]}}, sr, 16u * (uint32_t)i, {e0c * Z}, 0);")
+            w("        }")
+            w("    } else {")
+            w(f"        for (int i = t; i < {NE // 4}; i += {S.threads}) {{")
+            w("            const float4 v = reinterpret_cast<const float4*>(lds_all)[i];")
+            w("            __builtin_amdgcn_raw_buffer_store_b128(v4u{__float_as_uint(v.x), __float_as_uint(v.y), "
+              f"__float_as_uint(v.z), __float_as_uint(v.w)}}, sr, 16u * (uint32_t)i, {4 * e0c * Z}, 0);")
+            w("        }")
+            w("    }")
+            w("}")
+    elif not S.pipe:
         for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
             NE = (e1c - e0c) * Z
             w("template <int KIND>")
@@ -771,7 +807,13 @@ def emit(S: Spec) -> str:
         w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw, bool dup_, "
-          f"const float* lds_all) {{")
+          f"const float* lds_all{', int ub' if S.uremat else ''}) {{")
+        # UREMAT (the SAVE kernels of a one-codeword, unpadded geometry): the lane offsets u / vo / vc / vm are
+        # re-derived from the wave-uniform base ub and the lane id before each phase, so none of them lives across
+        # the iteration (the QMS training forward at the 128-VGPR cap spilled them and reloaded each phase with a
+        # vmcnt(0) wait -- behind every posterior / saved-state store in flight)
+        remat = ("        if constexpr (SAVE) { u = ub + lane_id(); vo = 4u * (uint32_t)u; vc = vo; vm = (uint32_t)u; }"
+                 if S.uremat else None)
         if S.pipe:
             w("    static_assert(MODE != 1, \"the SAVE kernels use the one-buffer schedule (save_c)\");")
         for i in range(Q):
@@ -859,6 +901,8 @@ def emit(S: Spec) -> str:
         w(f"        const rsrc_t pr = make_rsrc(pp ? pp + blk * {NZ} : a.xa, pp ? nlive * {4 * NZ} : 0);  // no output: stores dropped")
         w("        const uint8_t* pmp = (SAVE && a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t pm = make_rsrc((const float*)(pmp ? pmp + blk * {NZ} : nullptr), pmp ? nlive * {NZ} : 0);")
+        if remat:
+            w(remat)
         if "vn" not in SKIP:
             w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
@@ -910,15 +954,21 @@ def emit(S: Spec) -> str:
             declare_w(ci)
             w(f"        if constexpr (!({WLATE_COND}))")
             preload(ci)
+            if remat:
+                w(remat)
             w(f"        wr_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, it, sv, vc);")
 
         def op_cn(ci):
             w(f"        if constexpr ({WLATE_COND})")
             preload(ci)
+            if remat:
+                w(remat)
             if "cn" not in SKIP:
                 w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw, xr, apr, cdm);")
 
         def op_r(ci):
+            if remat:
+                w(remat)
             w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
               f"ps, d1m);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
@@ -933,7 +983,8 @@ def emit(S: Spec) -> str:
                 stamp(2 + 3 * ci)
                 w("        __syncthreads();")
                 # the image holds the chunk's v2c: save it before the check nodes overwrite it
-                w(f"        if constexpr (SAVE) {{ if (svb) save_c{ci}<KIND>(lds_all, svb, nlive, a.qp); __syncthreads(); }}")
+                tsave = f", {p * S.lanes} + ub + lane_id()" if S.uremat else ""
+                w(f"        if constexpr (SAVE) {{ if (svb) save_c{ci}<KIND>(lds_all, svb, nlive, a.qp{tsave}); __syncthreads(); }}")
                 op_cn(ci)
                 stamp(3 + 3 * ci)
                 w("        __syncthreads();")
@@ -964,6 +1015,8 @@ def emit(S: Spec) -> str:
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
         w("    const uint8_t* lmp = (SAVE && a.symask) ? a.symask + (a.T - 1) * a.symask_stride : nullptr;")
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
+        if remat:
+            w(remat)
         w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr);")
         w(f"    if constexpr (CNT) {{ if (dup_) ps.ec = 0; ps.{cnt_flush}({cnt_slot}, a.T - 1); }}")
         w("    if (a.c2v_out) {")
@@ -1002,8 +1055,10 @@ def emit(S: Spec) -> str:
     w(f"    __shared__ uint32_t app_all[{S.G_lds * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
     w(f"    uint32_t* appw = app_all + (dup_ ? {G} : g) * {S.N * S.WZX};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
-    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_, lds_all)",
-              indent="    ")
+    if S.uremat:
+        w("    const int ub = __builtin_amdgcn_readfirstlane(u - lane_id());  // (UREMAT) u of the wave's lane 0")
+    each_part("run_p{p}<KIND, MODE>(a, lds, u, blk, nlive, xr, vo, cr, vc, vm, cnt_all + g * 32, app_all, appw, dup_, lds_all"
+              + (", ub)" if S.uremat else ")"), indent="    ")
     w("    if constexpr (CNT) {")
     w("        __syncthreads();")
     w("        if (t < a.T) count_iteration(a, cnt_all, nlive, t);")

@@ -140,6 +140,9 @@ __device__ __forceinline__ float d1_v2c(float cd, const FusedArgs& a) {
 __device__ __forceinline__ void app_or(uint32_t* appw, int base, int v, bool bit) {
     if (bit) atomicOr(appw + base + (v >> 5), 1u << (v & 31));
 }
+// this lane's index in its wave (v_mbcnt: no register kept live for it)
+__device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
 
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
 // scalar loads (a row's edges are consecutive in C order: one s_load_dwordx8/x16 per row).

@@ -22,6 +22,9 @@ VARIANTS = [
     ("geom", {"NLDPC_GEN_GEOM": "bg2_z16:8,2,1"}, ["fused_bg2_z16_s0.hip", "fused_bg2_z16_bwd.hip"]),
     ("skip", {"NLDPC_GEN_SKIP": "sync,cnmath,d1post,wload,cnread,cnwrite"}, ["fused_bg2_z16_s3.hip"]),
     ("parts", {"NLDPC_GEN_PARTS": "1"}, ["fused_bg2_z16_s0.hip"]),
+    # (UREMAT applies to one-codeword geometries: BG2 z=384's training forward; z=16 packs 16 codewords)
+    ("uremat_off", {"NLDPC_GEN_UREMAT": "0", "NLDPC_GEN_ONLY": "bg2_z384", "NLDPC_GEN_KINDS": "3",
+                    "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z384_s1.hip"]),
 ]
 
 
@@ -57,5 +60,5 @@ def test_no_pruned_knob_is_read():
     src = open(os.path.join(CS, "gen_fused.py")).read()
     knobs = set(re.findall(r'environ\.get\("(NLDPC_[A-Z_0-9]+)"', src))
     assert knobs <= {"NLDPC_GEN_PARTS", "NLDPC_GEN_SKIP", "NLDPC_GEN_STAMPS", "NLDPC_GEN_GEOM", "NLDPC_GEN_WLATE",
-                     "NLDPC_GEN_NOBWD", "NLDPC_GEN_ONLY", "NLDPC_GEN_KINDS", "NLDPC_FUSED_EXTRA"}, knobs
+                     "NLDPC_GEN_NOBWD", "NLDPC_GEN_ONLY", "NLDPC_GEN_KINDS", "NLDPC_FUSED_EXTRA", "NLDPC_GEN_UREMAT"}, knobs
     assert len(knobs) <= 15

@@ -11,3 +11,8 @@ for c in ("fetch", "write"):
     for i, r in enumerate(rows):
         print(c, "kind", i, r["Counter_Name"], float(r["Counter_Value"]) * 1024 / 2**30, "GiB (KiB units)")
 PY
+cd $R && timeout -k 10 300 python bench.py --workload cfg2 --steps 200 --warmup 10 --no-cpu-baseline > $O/bench_cfg2_graph.log 2>&1 &&
+timeout -k 10 300 python bench.py --workload cfg2 --steps 200 --warmup 10 --no-cpu-baseline --graph off > $O/bench_cfg2_eager.log 2>&1 &&
+for f in bench_cfg2_graph bench_cfg2_eager; do python3 -c "
+import json; d=json.loads([l for l in open('$O/'+'$f'+'.log') if l.startswith('{')][-1])
+print('$f', d['value'], 'ms', d['ms_per_step'], 'median', d['ms_per_step_median'], 'kernel', d['roofline']['avg_launch_ms'], d['config'].get('graph'))"; done
