@@ -267,7 +267,7 @@ class Spec:
         # its busiest wave (a chain of LDS round trips, one per row copy), and whole rows balanced
         # badly: BG2 z=384 chunk 0 has 7 rows for 8 parts (edge copies per lane 30, 30, 24, 24, 18,
         # 18, 12, 0; by units at most 21)
-        # Register room: a unit's degree-1 edges stay in its part's registers for the whole decode (D1_BYPASS,
+        # Register room: a unit's degree-1 edges stay in its part's registers for the whole decode (the bypass,
         # `cd`), on top of the part's state; a part is offered a unit only while state + cd fits REG_ROOM (the
         # z=384 parts 0/1 hold 69/66 state floats), else the least-loaded part takes it anyway.
         d1e = {self.col_edges[j][0] for j in single}
@@ -310,23 +310,18 @@ def emit(S: Spec) -> str:
     w("#define SAVE (MODE == 1)")
     w("#define CNT (MODE >= 2)")
     w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
-    w("#define D1_BYPASS (!SAVE)")
     w("// check-row LDS addresses from one 32-bit base (ROADDR); in the QMS / SP kernels it measured slower")
     w("#define ROA (KIND == NLDPC_NEURAL || KIND == NLDPC_MS)")
     assert NZ < 65536  # per-codeword error counts are packed two to an LDS word
 
     # Register state of part p: one float array per lane copy q (cs{q}[slot]).  The channel values a thread
-    # needs every iteration are loaded once into registers (xs{q} for its register columns, xd for its
-    # degree-1 columns).
+    # needs every iteration are loaded once into registers (xs{q} for its register columns; those of the
+    # degree-1 columns are held by the check-node threads, cd).
     def ref(p, q, k):
         return f"cs{q}[{k}]"
 
     def xref(p, j, q):
-        cols = S.reg_cols[p]
-        if j in cols:
-            return f"xs{q}[{cols.index(j)}]"
-        n = S.d1_cols[p].index(j)
-        return f"xd[{n * Q + q}]"
+        return f"xs{q}[{S.reg_cols[p].index(j)}]"
 
     def state_params(p, const=False):
         sp = len(S.slots[p])
@@ -337,20 +332,16 @@ def emit(S: Spec) -> str:
         return ", ".join(f"cs{i}" for i in range(Q))
 
     def x_params(p):
-        nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
-        ps = [f"const float (&xs{i})[{nr}]" for i in range(Q)]
-        ps.append(f"const float (&xd)[{nd}]")
-        return ", ".join(ps)
+        nr = max(len(S.reg_cols[p]), 1)
+        return ", ".join(f"const float (&xs{i})[{nr}]" for i in range(Q))
 
     def x_args(p):
-        return ", ".join([f"xs{i}" for i in range(Q)] + ["xd"])
+        return ", ".join(f"xs{i}" for i in range(Q))
 
-    # UCN hard decisions a thread keeps in registers: d1m (its degree-1 columns' posteriors, the non-bypass
-    # kernels) and cdm (bypass: the posteriors of its cd entries) -- bit arrays of 32-bit words, as many as the
-    # part needs (a run-time geometry with few parts can hold more than 32)
-    def nwords(p, which):
-        n = len(S.d1_cols[p]) * Q if which == "d1m" else len(S.cd_index[p])
-        return max(1, -(-n // 32))
+    # UCN hard decisions of the posteriors of a thread's cd entries (cdm) -- a bit array of 32-bit words, as many
+    # as the part needs (a run-time geometry with few parts can hold more than 32)
+    def nwords(p):
+        return max(1, -(-len(S.cd_index[p]) // 32))
 
     def bit_get(arr, b):
         return f"({arr}[{b >> 5}] >> {b & 31})"
@@ -436,7 +427,7 @@ def emit(S: Spec) -> str:
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void {fname}({state_params(p)}, {x_params(p)}, const FusedArgs& a, "
               f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t* appw, int u, "
-              f"const uint32_t (&d1m)[{nwords(p, 'd1m')}], rsrc_t apr) {{")
+              f"rsrc_t apr) {{")
             if not final:
                 w("    const bool ucn_ = KIND != NLDPC_NEURAL && a.ucn;  // UCN: hard decisions of the previous posterior")
             # every posterior's xa (cumulative VN weights) requested before the first posterior store: a later
@@ -468,16 +459,7 @@ def emit(S: Spec) -> str:
                 w("        }")
                 w("        __builtin_amdgcn_sched_barrier(0);")
                 s += d
-            if not final and S.d1_cols[p]:
-                # degree-1 columns: their posterior of iteration it-1 was formed in that iteration's read-back
-                # (rd_p), its hard decision kept in d1m (bypass: in the check-node thread's cdm instead)
-                w("    if (!D1_BYPASS && ucn_) {")
-                for n, j in enumerate(S.d1_cols[p]):
-                    for q in range(Q):
-                        app0 = f"(a.first_iter > 0 ? bload(apr, vo, {X(j, q)}) : chan<KIND>(xd[{n * Q + q}], a))"
-                        bit = f"it == 0 ? {app0} >= 0.f : ({bit_get('d1m', n * Q + q)} & 1u) != 0u"
-                        w(f"        app_or(appw, {j * S.WZX}, u + {q * ZT}, {bit});")
-                w("    }")
+            # (degree-1 columns: their UCN hard decisions are the check-node threads' own, cdm)
             w("}")
 
     # ---------------------------------------------------------------- LDS chunk write / read-back
@@ -497,7 +479,8 @@ def emit(S: Spec) -> str:
     for p in range(S.P):
         for ci, (r0, r1, e0, e1) in enumerate(S.chunks):
             mine = [(k, e) for k, e in enumerate(S.slots[p]) if e0 <= e < e1]
-            d1 = [(j, S.col_edges[j][0]) for j in S.d1_cols[p] if e0 <= S.col_edges[j][0] < e1]
+            # (degree-1 edges never enter the image: their check-node threads form their v2c, posteriors, clamp
+            # masks, saved v2c and xin themselves -- cn_p)
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void wr_p{p}_c{ci}({state_params(p, True)}, {x_params(p)}, float* lds, "
               f"int u, const FusedArgs& a, int it, rsrc_t sv, uint32_t vc) {{")
@@ -505,55 +488,26 @@ def emit(S: Spec) -> str:
             for q in range(Q):
                 for k, e in mine:
                     w(f"    {own_lv(e, q, e0)} = {ref(p, q, k)};")
-            if d1:  # v2c = (0 + xin) + 0: no other edge in the column (bypass: the check node reads xa)
-                w("    if constexpr (!D1_BYPASS) {")
-            for j, e in d1:
-                for q in range(Q):
-                    w(f"    {{ const float v_ = fadd(fadd(0.f, chan<KIND>({xref(p, j, q)}, a)), 0.f); {own_lv(e, q, e0)} = v_; }}")
-            if d1:
-                w("    }")
             w("}")
             w("template <int KIND, int MODE>")
             w(f"__device__ __forceinline__ void rd_p{p}_c{ci}({state_params(p)}, {x_params(p)}, const float* lds, "
               f"int u, const FusedArgs& a, uint32_t vo, rsrc_t pr, rsrc_t cr, uint32_t vc, bool has_co, "
-              f"uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t (&d1m)[{nwords(p, 'd1m')}]) {{")
+              f"uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
             for q in range(Q):
                 for k, e in mine:
                     w(f"    {ref(p, q, k)} = {own_lv(e, q, e0)};")
-            if d1:  # this iteration's posterior right away (bypass: written by the check node)
-                w("    if constexpr (!D1_BYPASS) {")
-            for j, e in d1:
-                for q in range(Q):
-                    w(f"    const float xl_{j}_{q} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, q)}) : {xref(p, j, q)};")
-            for j, e in d1:
-                for q in range(Q):
-                    bit = S.d1_cols[p].index(j) * Q + q
-                    w(f"    {{ const float xo_ = xl_{j}_{q};")
-                    w(f"      const float P_ = fadd(0.f, {own_lv(e, q, e0)});")
-                    w("      float y_;")
-                    w("      if constexpr (SAVE && KIND != NLDPC_NEURAL) {")
-                    w(f"          bool m_; y_ = posterior_m<KIND>(xo_, P_, a, m_); bstore(pr, vo, {X(j, q)}, y_); "
-                      f"bstore8(pm, vm, {X(j, q) // 4}, m_);")
-                    w(f"      }} else {{ y_ = posterior<KIND>(xo_, P_, a); put_post<CM>(pr, vo, {X(j, q)}, y_, ps); }}")
-                    w(f"      if (KIND != NLDPC_NEURAL && a.ucn) {bit_set('d1m', bit, 'y_ >= 0.f')}; }}")
-            if d1:
-                w("    if (has_co) {  // final message state (last iteration only)")
-                for j, e in d1:
-                    for q in range(Q):
-                        w(f"        bstore(cr, vc, {4 * (e * Z + q * ZT)}, {own_lv(e, q, e0)});")
-                w("    }")
-                w("    }")
             w("}")
 
     # ---------------------------------------------------------------- check nodes
     # LDS holds each edge's Z messages in CHECK order (the owners rotate on write/read-back), so the
     # thread of check copy h reads every edge of its row at h: one address per row copy, the edges at
     # immediate offsets k*Z.  Rows are emitted inline per part and chunk (literal edges and degree).
-    # D1_BYPASS (Neural inference): a degree-1 edge's v2c is the channel value itself, so instead of a
-    # round trip owner -> LDS -> check node -> LDS -> owner, the check-node thread keeps that edge's xa
-    # (at its rotated copies) in registers from the start and writes the edge's posterior (and final
-    # c2v) itself: ~19% of the LDS traffic of BG2 (38 of 197 edges) disappears.
+    # Degree-1 bypass (every kernel; the training forward since r5): a degree-1 edge's v2c is its channel value
+    # itself, so instead of a round trip owner -> LDS -> check node -> LDS -> owner, the check-node thread keeps
+    # that edge's xa (at its rotated copies, advanced by the cumulative VN weights) in registers from the start
+    # and writes the edge's posterior (and final c2v; training: its saved v2c, clamp mask and xin) itself:
+    # ~19% of the LDS traffic of BG2 (38 of 197 edges) disappears.
     d1set = {S.col_edges[j][0] for j in range(S.N) if len(S.col_edges[j]) == 1}
     S.cd_index = {}  # part -> list of (edge, q) whose xa the check-node thread holds
     for p in range(S.P):
@@ -584,7 +538,8 @@ def emit(S: Spec) -> str:
             w(f"__device__ __forceinline__ void cn_p{p}_c{ci}(float* lds, int u, const FusedArgs& a, int it, "
               f"const float (&cd)[{ncd}], uint32_t vo, rsrc_t nr, rsrc_t cr, uint32_t vc, bool co_last, "
               f"const float (&W)[{S.cn_nw[(p, ci)]}], const float (&Bv)[{S.cn_nw[(p, ci)]}], PostSink& ps, "
-              f"const uint32_t* appw, rsrc_t xr, rsrc_t apr, uint32_t (&cdm)[{nwords(p, 'cdm')}]) {{")
+              f"const uint32_t* appw, rsrc_t xr, rsrc_t apr, uint32_t (&cdm)[{nwords(p)}]"
+              f", rsrc_t sv, rsrc_t nm, rsrc_t sxd) {{")
             w("    asm volatile(\"\" : \"+v\"(u));")
             w("    const uint32_t lu_ = (uint32_t)(uintptr_t)(lds_fp)lds + 4u * (uint32_t)u;")
             # row copies in order; weight offsets of each row in the preloaded W/Bv arrays
@@ -618,8 +573,7 @@ def emit(S: Spec) -> str:
                 w("    }")
                 for k, e in enumerate(es):
                     if e in d1set:
-                        w(f"    if constexpr (D1_BYPASS) m{n}[{k}] = d1_v2c<KIND, 1>(cd[{S.cd_index[p].index((e, q))}], a); "
-                          f"else m{n}[{k}] = rq{n}[{off[e]}];")
+                        w(f"    m{n}[{k}] = d1_v2c<KIND, 1>(cd[{S.cd_index[p].index((e, q))}], a);")
                     elif "cnread" in SKIP:  # (timing experiment: no check-node LDS reads, junk inputs)
                         w(f"    m{n}[{k}] = __uint_as_float(0x3f800000u + ((uint32_t)u << 8) + {k * 977 + n * 131}u);")
                     else:
@@ -631,6 +585,16 @@ def emit(S: Spec) -> str:
                 DC = len(es)
                 _, off = row_slots(i)
                 w("    {")
+                # SAVE: the row copy's v2c, as read, into the saved [E][Z] image by check copy h = u + q*ZT (r5: the
+                # check-node threads store it from their registers; before, the whole workgroup copied each chunk
+                # image between two extra barriers)
+                w("        if constexpr (SAVE) {")
+                # (one-codeword geometries: the codeword's element offset is u itself, no other value kept live)
+                eo = "(uint32_t)u" if S.uremat else "(vc >> 2)"
+                for k, e in enumerate(es):
+                    w(f"            if constexpr (KIND == NLDPC_QMS) bstore_i8(sv, {eo} + {q * ZT}u, {e * Z}, qms_code_p(m{n}[{k}], a.qp));")
+                    w(f"            else bstore(sv, 4u * {eo} + {4 * q * ZT}u, {4 * e * Z}, m{n}[{k}]);")
+                w("        }")
                 w(f"        float wv[{DC}], bv[{DC}];")
                 w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{woff[i]} + k]; bv[k] = Bv[{woff[i]} + k]; }}")
                 w("        const bool wc = a.w_cn != nullptr;")
@@ -652,13 +616,10 @@ def emit(S: Spec) -> str:
                         continue
                     c, dvu = rot(e, q)
                     j = int(S.hb_cols[e])
-                    vexpr = f"u + {c}" if c + ZT <= Z else f"u + {c} - (u >= {Z - c} ? {Z} : 0)"
-                    rd_ = f"{{ const int v_ = {vexpr}; par_ ^= appw[{j * S.WZX} + (v_ >> 5)] >> (v_ & 31); }}"
-                    # bypass: the hard decision of this thread's own previous posterior
+                    # the hard decision of this thread's own previous posterior of that edge's column copy
                     ix = S.cd_index[p].index((e, q))
                     app0 = f"(a.first_iter > 0 ? bload(apr, vo + {dvu}, {4 * (j * Z + c)}) : chan<KIND>(cd[{ix}], a))"
-                    w(f"            if constexpr (D1_BYPASS) par_ ^= it == 0 ? ({app0} >= 0.f ? 1u : 0u) : {bit_get('cdm', ix)}; "
-                      f"else {rd_}")
+                    w(f"            par_ ^= it == 0 ? ({app0} >= 0.f ? 1u : 0u) : {bit_get('cdm', ix)};")
                 w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
                 w("        }")
                 if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
@@ -669,13 +630,18 @@ def emit(S: Spec) -> str:
                         c, dv = rot(e, q)
                         ix = S.cd_index[p].index((e, q))
                         pm = f"fadd(0.f, m{n}[{k}])"
-                        w("        if constexpr (D1_BYPASS) {")
+                        w("        {")
                         w(f"            const uint32_t dv_ = {dv};")
                         w("            float y_;")
                         w(f"            if constexpr (KIND == NLDPC_NEURAL) y_ = fadd(cd[{ix}], {pm});")
                         w("            else {  // Boosted: the unweighted channel value (cumulative VN weights: from memory)")
                         w(f"                const float xo_ = a.w_vn ? bload(xr, vo + dv_, {4 * (j * Z + c)}) : cd[{ix}];")
-                        w(f"                y_ = posterior<KIND>(xo_, {pm}, a);")
+                        # the training forward: the clamp mask (byte offset = the float offset / 4) and this
+                        # iteration's xin too (the owners keep no degree-1 state)
+                        w("                if constexpr (SAVE) { bool m_; "
+                          f"y_ = posterior_m<KIND>(xo_, {pm}, a, m_); bstore8(nm, (vo + dv_ + {4 * (j * Z + c)}u) >> 2, 0, m_); "
+                          f"bstore(sxd, vo + dv_, {4 * (j * Z + c)}, cd[{ix}]); }}")
+                        w(f"                else y_ = posterior<KIND>(xo_, {pm}, a);")
                         w(f"                if (a.ucn) {bit_set('cdm', ix, 'y_ >= 0.f')};")
                         w("            }")
                         if "d1post" in SKIP:  # (timing experiment: no degree-1 posterior stores)
@@ -683,7 +649,7 @@ def emit(S: Spec) -> str:
                         else:
                             w(f"            put_post<CM>(nr, vo + dv_, {4 * (j * Z + c)}, y_, ps);")
                         w(f"            if (co_last) bstore(cr, vc + dv_, {4 * (e * Z + c)}, m{n}[{k}]);")
-                        w(f"        }} else {{ rq{n}[{off[e]}] = m{n}[{k}]; }}")
+                        w("        }")
                     elif "cnwrite" in SKIP:  # (timing experiment: keep the value live without the LDS write)
                         w(f"        asm volatile(\"\" :: \"v\"(m{n}[{k}]));")
                     else:
@@ -699,80 +665,6 @@ def emit(S: Spec) -> str:
                     rc_load(n + 1)
                 w("    __builtin_amdgcn_sched_barrier(0);")
                 rc_compute(n)
-            w("}")
-
-    # ---------------------------------------------------------------- SAVE: chunk image -> saved v2c
-    # The image of chunk c is [G][CF] floats in check order: edge e0+i's message for check copy h at
-    # i*Z + h, the saved buffer's layout for this codeword's edges e0..e1 (nldpc_forward.hip).  Every
-    # thread of the workgroup copies 16-byte pieces (QMS: 16 messages -> 16 int8 codes).
-    if not S.pipe and S.uremat:
-        # (UREMAT: the thread index re-derived by the caller, stores through a buffer descriptor with 32-bit
-        # offsets instead of 64-bit flat addresses -- one codeword per workgroup, 16-byte aligned chunks)
-        for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
-            NE = (e1c - e0c) * Z
-            assert NE % 16 == 0 and (e0c * Z) % 16 == 0 and (S.E * Z) % 16 == 0 and G == 1
-            w("template <int KIND>")
-            w(f"__device__ __forceinline__ void save_c{ci}(const float* lds_all, char* svb, int nlive, const QParams& qp, int t) {{")
-            w("    (void)qp; (void)nlive;")
-            w("    typedef uint32_t v4u __attribute__((ext_vector_type(4)));")
-            w(f"    const rsrc_t sr = make_rsrc((const float*)svb, {S.E * Z} * saved_msg_bytes<KIND>());  // this codeword's saved block")
-            w("    if constexpr (KIND == NLDPC_QMS) {")
-            w(f"        for (int i = t; i < {NE // 16}; i += {S.threads}) {{")
-            w("            const float4* s4 = (const float4*)(lds_all + 16 * i);")
-            w("            uint32_t o[4];")
-            w("#pragma unroll")
-            w("            for (int k = 0; k < 4; ++k) {")
-            w("                const float4 v = s4[k];")
-            w("                o[k] = ((uint32_t)qms_code_p(v.x, qp) & 255u) | (((uint32_t)qms_code_p(v.y, qp) & 255u) << 8) |")
-            w("                       (((uint32_t)qms_code_p(v.z, qp) & 255u) << 16) | ((uint32_t)qms_code_p(v.w, qp) << 24);")
-            w("            }")
-            w(f"            __builtin_amdgcn_raw_buffer_store_b128(v4u{{o[0], o[1], o[2], o[3]}}, sr, 16u * (uint32_t)i, {e0c * Z}, 0);")
-            w("        }")
-            w("    } else {")
-            w(f"        for (int i = t; i < {NE // 4}; i += {S.threads}) {{")
-            w("            const float4 v = reinterpret_cast<const float4*>(lds_all)[i];")
-            w("            __builtin_amdgcn_raw_buffer_store_b128(v4u{__float_as_uint(v.x), __float_as_uint(v.y), "
-              f"__float_as_uint(v.z), __float_as_uint(v.w)}}, sr, 16u * (uint32_t)i, {4 * e0c * Z}, 0);")
-            w("        }")
-            w("    }")
-            w("}")
-    elif not S.pipe:
-        for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
-            NE = (e1c - e0c) * Z
-            w("template <int KIND>")
-            w(f"__device__ __forceinline__ void save_c{ci}(const float* lds_all, char* svb, int nlive, const QParams& qp) {{")
-            w("    const int t = threadIdx.x;")
-            w("    (void)qp;")
-            for g in range(G):
-                src = f"(lds_all + {g * S.cw_floats})"
-                w(f"    if ({g} < nlive) {{")
-                w("        if constexpr (KIND == NLDPC_QMS) {")
-                w(f"            int8_t* dst = (int8_t*)(svb + {(g * S.E + e0c) * Z});")
-                # 16-byte stores only where every absolute address is 16-byte aligned: the saved buffer
-                # is 256-byte aligned, and iteration / block / codeword strides are multiples of E*Z bytes
-                if NE % 16 == 0 and (g * S.cw_floats) % 4 == 0 and ((g * S.E + e0c) * Z) % 16 == 0 and (S.E * Z) % 16 == 0:
-                    w(f"            for (int i = t; i < {NE // 16}; i += {S.threads}) {{")
-                    w(f"                const float4* s4 = (const float4*)({src} + 16 * i);")
-                    w("                uint32_t o[4];")
-                    w("#pragma unroll")
-                    w("                for (int k = 0; k < 4; ++k) {")
-                    w("                    const float4 v = s4[k];")
-                    w("                    o[k] = ((uint32_t)qms_code_p(v.x, qp) & 255u) | (((uint32_t)qms_code_p(v.y, qp) & 255u) << 8) |")
-                    w("                           (((uint32_t)qms_code_p(v.z, qp) & 255u) << 16) | ((uint32_t)qms_code_p(v.w, qp) << 24);")
-                    w("                }")
-                    w("                reinterpret_cast<uint4*>(dst)[i] = make_uint4(o[0], o[1], o[2], o[3]);")
-                    w("            }")
-                else:
-                    w(f"            for (int i = t; i < {NE}; i += {S.threads}) dst[i] = (int8_t)qms_code_p({src}[i], qp);")
-                w("        } else {")
-                w(f"            float* dst = (float*)(svb + {4 * (g * S.E + e0c) * Z});")
-                if NE % 4 == 0 and (g * S.cw_floats) % 4 == 0 and ((g * S.E + e0c) * Z) % 4 == 0 and (S.E * Z) % 4 == 0:
-                    w(f"            for (int i = t; i < {NE // 4}; i += {S.threads}) "
-                      f"reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>({src})[i];")
-                else:
-                    w(f"            for (int i = t; i < {NE}; i += {S.threads}) dst[i] = {src}[i];")
-                w("        }")
-                w("    }")
             w("}")
 
     # ---------------------------------------------------------------- the kernel
@@ -803,7 +695,7 @@ def emit(S: Spec) -> str:
         if PARTS and p not in PARTS:
             continue
         sp = max(len(S.slots[p]), 1)
-        nr, nd = max(len(S.reg_cols[p]), 1), max(len(S.d1_cols[p]) * Q, 1)
+        nr = max(len(S.reg_cols[p]), 1)
         w("template <int KIND, int MODE>")
         w(f"__device__ __forceinline__ void run_p{p}(const FusedArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"rsrc_t xr, uint32_t vo, rsrc_t cr, uint32_t vc, uint32_t vm, int* cntl, uint32_t* app_all, uint32_t* appw, bool dup_, "
@@ -814,11 +706,10 @@ def emit(S: Spec) -> str:
         # vmcnt(0) wait -- behind every posterior / saved-state store in flight)
         remat = ("        if constexpr (SAVE) { u = ub + lane_id(); vo = 4u * (uint32_t)u; vc = vo; vm = (uint32_t)u; }"
                  if S.uremat else None)
-        if S.pipe:
-            w("    static_assert(MODE != 1, \"the SAVE kernels use the one-buffer schedule (save_c)\");")
+        if S.pipe:  # (r2: the pipelined schedule made the training forward slower; r5 with the check-node saves: still)
+            w("    static_assert(MODE != 1, \"the SAVE kernels use the one-buffer schedule\");")
         for i in range(Q):
             w(f"    float cs{i}[{sp}], xs{i}[{nr}];")
-        w(f"    float xd[{nd}];")
         w("#pragma unroll")
         w(f"    for (int k = 0; k < {sp}; ++k) {{")
         for i in range(Q):
@@ -828,21 +719,18 @@ def emit(S: Spec) -> str:
         for n, j in enumerate(S.reg_cols[p]):
             for i in range(Q):
                 w(f"    xs{i}[{n}] = bload(xr, vo, {X(j, i)});")
-        for n, j in enumerate(S.d1_cols[p]):
-            for q in range(Q):
-                w(f"    xd[{n * Q + q}] = bload(xr, vo, {X(j, q)});")
         w(f"    PostSink ps{{make_rsrc((const float*)(a.cnt_y ? a.cnt_y + blk * {NZ} : nullptr), "
           f"a.cnt_y ? nlive * {NZ} : 0), 0, a.cnt_conv}};")
         ncd = max(len(S.cd_index[p]), 1)
-        w(f"    float cd[{ncd}];  // D1_BYPASS: xa of the degree-1 edges of this part's check rows, rotated copies")
-        w("    if constexpr (D1_BYPASS) {")
+        w(f"    float cd[{ncd}];  // xa of the degree-1 edges of this part's check rows, rotated copies")
+        w("    {")
         for idx, (e, q) in enumerate(S.cd_index[p]):
             c, dv = rot(e, q)
             # (0 + xa): the v2c of a degree-1 edge, canonical (never -0), as the check node sees it
             w(f"        {{ const float x_ = bload(xr, vo + {dv}, {4 * (int(S.hb_cols[e]) * Z + c)}); "
               f"cd[{idx}] = KIND == NLDPC_NEURAL ? fadd(0.f, x_) : x_; }}")
-        w("    } else {")
-        w(f"        for (int k = 0; k < {ncd}; ++k) cd[k] = 0.f;")
+        if not S.cd_index[p]:
+            w("        cd[0] = 0.f;")
         w("    }")
         # cumulative VN weighting: the channel registers hold xin and advance one step per iteration
         def chan_steps(step_expr, indent):
@@ -850,11 +738,8 @@ def emit(S: Spec) -> str:
             for n, j in enumerate(S.reg_cols[p]):
                 for i in range(Q):
                     w(f"{indent}  xs{i}[{n}] = chan_step<KIND>(xs{i}[{n}], a, wr_[{j}]);")
-            for n, j in enumerate(S.d1_cols[p]):
-                for q in range(Q):
-                    w(f"{indent}  xd[{n * Q + q}] = chan_step<KIND>(xd[{n * Q + q}], a, wr_[{j}]);")
-            if S.cd_index[p]:  # (bypass: the degree-1 channel values the check-node thread holds)
-                w(f"{indent}  if constexpr (D1_BYPASS) {{")
+            if S.cd_index[p]:  # (the degree-1 channel values the check-node thread holds)
+                w(f"{indent}  {{")
                 for idx, (e, q) in enumerate(S.cd_index[p]):
                     w(f"{indent}    cd[{idx}] = chan_step<KIND>(cd[{idx}], a, wr_[{int(S.hb_cols[e])}]);")
                 w(f"{indent}  }}")
@@ -875,8 +760,7 @@ def emit(S: Spec) -> str:
                   f"__builtin_amdgcn_s_memtime();")
         # UCN: the hard-decision bit array of the codewords starts at zero (bits are OR-ed in); every later
         # iteration's array is cleared in the read-back phase of the iteration before
-        w(f"    uint32_t d1m[{nwords(p, 'd1m')}] = {{}};  // UCN: hard decisions of this thread's degree-1 posteriors")
-        w(f"    uint32_t cdm[{nwords(p, 'cdm')}] = {{}};  // UCN, D1_BYPASS: hard decisions of the posteriors of its cd entries")
+        w(f"    uint32_t cdm[{nwords(p)}] = {{}};  // UCN: hard decisions of the posteriors of its cd entries")
         w(f"    const rsrc_t apr = make_rsrc(a.app_prev ? a.app_prev + blk * {NZ} : a.xa, a.app_prev ? nlive * {4 * NZ} : 0);")
         w("    if (KIND != NLDPC_NEURAL && a.ucn) {")
         w(f"        for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
@@ -892,11 +776,11 @@ def emit(S: Spec) -> str:
         for n, j in enumerate(S.reg_cols[p]):
             for q in range(Q):
                 w(f"                bstore(sx, vo, {X(j, q)}, {xref(p, j, q)});")
-        for n, j in enumerate(S.d1_cols[p]):
-            for q in range(Q):
-                w(f"                bstore(sx, vo, {X(j, q)}, {xref(p, j, q)});")
         w("            }")
         w("        }")
+        # (the check-node threads store the degree-1 columns' xin: cn_p)
+        w("        float* sxd_ = (SAVE && KIND != NLDPC_NEURAL && a.w_vn && a.sxin) ? a.sxin + it * a.sxin_stride : nullptr;")
+        w(f"        const rsrc_t sxd = make_rsrc(sxd_ ? sxd_ + blk * {NZ} : a.xa, sxd_ ? nlive * {4 * NZ} : 0);")
         w("        const float* pp = it >= 1 ? a.outs.p[it - 1] : nullptr;  // previous iteration's posterior")
         w(f"        const rsrc_t pr = make_rsrc(pp ? pp + blk * {NZ} : a.xa, pp ? nlive * {4 * NZ} : 0);  // no output: stores dropped")
         w("        const uint8_t* pmp = (SAVE && a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
@@ -904,7 +788,7 @@ def emit(S: Spec) -> str:
         if remat:
             w(remat)
         if "vn" not in SKIP:
-            w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, d1m, apr);")
+            w(f"        vn_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, it, pr, vm, xr, pm, ps, appw, u, apr);")
         # iteration it-1 is complete (at it = 0 the VN step made no output: nothing to count)
         w(f"        if constexpr (CNT) {{ if (dup_) ps.ec = 0; if (it >= 1) ps.{cnt_flush}({cnt_slot}, it - 1); else ps.ec = 0; }}")
         w("        const float* pn = a.outs.p[it];  // this iteration's posterior (degree-1 columns)")
@@ -915,8 +799,7 @@ def emit(S: Spec) -> str:
         w("        const char* svp = SAVE ? a.sv2c + it * a.sv2c_stride * SB : nullptr;")
         w(f"        const rsrc_t sv = make_rsrc((const float*)(svp ? svp + blk * {S.E * Z} * SB : nullptr), "
           f"svp ? nlive * {S.E * Z} * SB : 0);")
-        w(f"        char* svb = svp ? const_cast<char*>(svp) + blk * {S.E * Z} * SB : nullptr;  // (save_c)")
-        w("        (void)sv; (void)svb;")
+        w("        (void)sv;")
         w("        const bool co_last = a.c2v_out && it == a.T - 1;")
         stamp(1)
         def declare_w(ci):
@@ -964,13 +847,13 @@ def emit(S: Spec) -> str:
             if remat:
                 w(remat)
             if "cn" not in SKIP:
-                w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw, xr, apr, cdm);")
+                w(f"        cn_p{p}_c{ci}<KIND, MODE>({buf(ci)}, u, a, it, cd, vo, nr, cr, vc, co_last, W{ci}, B{ci}, ps, appw, xr, apr, cdm, sv, nm, sxd);")
 
         def op_r(ci):
             if remat:
                 w(remat)
             w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
-              f"ps, d1m);")
+              f"ps);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
                 w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
                 w(f"            for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
@@ -982,9 +865,6 @@ def emit(S: Spec) -> str:
                 op_w(ci)
                 stamp(2 + 3 * ci)
                 w("        __syncthreads();")
-                # the image holds the chunk's v2c: save it before the check nodes overwrite it
-                tsave = f", {p * S.lanes} + ub + lane_id()" if S.uremat else ""
-                w(f"        if constexpr (SAVE) {{ if (svb) save_c{ci}<KIND>(lds_all, svb, nlive, a.qp{tsave}); __syncthreads(); }}")
                 op_cn(ci)
                 stamp(3 + 3 * ci)
                 w("        __syncthreads();")
@@ -1017,7 +897,7 @@ def emit(S: Spec) -> str:
         w(f"    const rsrc_t lm = make_rsrc((const float*)(lmp ? lmp + blk * {NZ} : nullptr), lmp ? nlive * {NZ} : 0);")
         if remat:
             w(remat)
-        w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, d1m, apr);")
+        w(f"    post_p{p}<KIND, MODE>({state_args(p)}, {x_args(p)}, a, vo, a.T, lr, vm, xr, lm, ps, appw, u, apr);")
         w(f"    if constexpr (CNT) {{ if (dup_) ps.ec = 0; ps.{cnt_flush}({cnt_slot}, a.T - 1); }}")
         w("    if (a.c2v_out) {")
         for q in range(Q):
@@ -1068,7 +948,6 @@ def emit(S: Spec) -> str:
     w(f"__global__ __launch_bounds__({S.threads}, {(S.threads + 255) // 256}) void kernel(FusedArgs a) {{")
     w("    kernel_body<KIND, MODE>(a);")
     w("}")
-    w("#undef D1_BYPASS")
     w("#undef ROA")
     w("#undef SAVE")
     w("#undef CNT")
