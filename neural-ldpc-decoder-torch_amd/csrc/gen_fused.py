@@ -1156,7 +1156,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     w("                gwa[k] += gw[k];")
     w("            }")
     w("        } else {")
-    w("            cn_bwd_ms<DC, KIND>(load_m, rp + q * ZT, Z, wv, bv, KIND == NLDPC_NEURAL || wc, a.qbit, a.lo, a.hi, "
+    w("            cn_bwd_ms<DC, KIND, TIED != 0>(load_m, rp + q * ZT, Z, wv, bv, KIND == NLDPC_NEURAL || wc, a.qbit, a.lo, a.hi, "
       "gwa, gba);")
     w("        }")
     def flush_q(indent):  # this copy's wave sums, added up over the row's copies by lane 0 in LDS

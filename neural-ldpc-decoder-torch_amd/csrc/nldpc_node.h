@@ -474,7 +474,11 @@ __device__ __forceinline__ void cn_backward(const float (&m)[DC], const float (&
 // them.  load_m(k) gives edge k's v2c input (QMS: the decoded int8 code of the saved state, with an
 // active quantiser); lds[k * stride] holds dL/dc2v on entry and receives
 // dL/dv2c.  gwa / gba accumulate this copy's dL/dw_cn and dL/dbias contributions.
-template <int DC, int KIND, typename LoadM>
+// SAMEW (the tied-weight kernel: one CN weight for the whole row): every edge but the first-index argmin
+// has the same magnitude, so the epilogue's masks take two values per row, computed once (the same
+// operations on the same values as per edge: the results are bit-identical), and the weight gradient is one
+// running sum in gwa[0] (r5: cfg5 backward 27.3 -> 26.5 ms, profiles/r5o_ab_tied_bwd_masks.txt).
+template <int DC, int KIND, bool SAMEW = false, typename LoadM>
 __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride, const float (&wc)[DC],
                                           const float (&bb)[DC], bool has_w, int qbit, float lo, float hi,
                                           float (&gwa)[DC], float (&gba)[DC]) {
@@ -512,6 +516,42 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
         }
     }
     float g_at1 = 0.f, g_at2 = 0.f;
+    if constexpr (SAMEW && KIND != NLDPC_NEURAL) {
+        // A: every edge but idx1 (magnitude min1), B: edge idx1 (min2); the zero-fix correction, x1 = |x| w
+        // (|x| = |mag|: x = mag * (+-1)), the clip / quantiser mask of relu(x1) and the relu mask, per row
+        const float magA = (min1 > kZeroFix) ? min1 : fadd(min1, -kZeroFix);
+        const float magB = (min2 > kZeroFix) ? min2 : fadd(min2, -kZeroFix);
+        const float x1A = has_w ? fmul(fabsf(magA), wc[0]) : fabsf(magA);
+        const float x1B = has_w ? fmul(fabsf(magB), wc[0]) : fabsf(magB);
+        // (g2 * mq) * mp == g2 * (mq * mp) bit for bit when both masks are 0 or 1: one mask per case
+        const bool qmask = KIND == NLDPC_MS || qr.active;
+        const float mqA = !qmask ? 1.f : KIND == NLDPC_QMS ? in_range(relu_mask(x1A), qr.lo, qr.hi) : in_range(relu_mask(x1A), lo, hi);
+        const float mqB = !qmask ? 1.f : KIND == NLDPC_QMS ? in_range(relu_mask(x1B), qr.lo, qr.hi) : in_range(relu_mask(x1B), lo, hi);
+        const float mA = (x1A > 0.f) ? mqA : 0.f, mB = (x1B > 0.f) ? mqB : 0.f;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const bool sel = k == idx1;
+            const float mag = sel ? magB : magA;
+            const float sgn = ((npos ^ (posm >> k)) & 1u) ? 1.f : -1.f;
+            const float x = fmul(mag, sgn);
+            const float s = signf_t(x), ax = fabsf(x);
+            const float gc = lds[k * stride];
+            const float g1 = (gc * s) * (sel ? mB : mA);
+            float gabs;
+            if (!has_w) {
+                gabs = g1;
+            } else {
+                // one running sum in gwa[0] instead of one per edge: the tied kernel adds gwa[0..DC-1] in edge
+                // order from 0 (cnb_row), and 0 + ... + g1_k ax_k in edge order is that sum bit for bit (a
+                // partial sum from +0 is never -0, so adding +-0 terms directly or as 0 + term is the same)
+                gwa[0] += g1 * ax;
+                gabs = g1 * wc[k];
+            }
+            const float gmag = (gabs * s) * sgn;
+            if (sel) g_at2 += gmag;
+            else g_at1 += gmag;
+        }
+    } else {
 #pragma unroll
     for (int k = 0; k < DC; ++k) {  // pass 2: epilogue backward per edge (cn_backward's formulas)
         float mag = (k == idx1) ? min2 : min1;
@@ -545,6 +585,7 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
         const float gmag = (gabs * s) * sgn;
         if (k == idx1) g_at2 += gmag;
         else g_at1 += gmag;
+    }
     }
 #pragma unroll
     for (int l = 0; l < DC; ++l) {  // pass 3: the two argmins receive the gradient
