@@ -74,8 +74,6 @@ NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"  # experiment builds without ba
 # SAVE kernels of one-codeword geometries: lane offsets re-derived per phase, buffer-descriptor saves (r5: the
 # cfg5 training forward 11.57 -> 11.38 ms, profiles/r5i_ab_uremat.txt); NLDPC_GEN_UREMAT=0 turns it off
 UREMAT = os.environ.get("NLDPC_GEN_UREMAT", "1") == "1"
-# (r5 A/B) with UREMAT: the SAVE kernel's LDS bases (image, UCN bits) wave-uniform, as the backward's (LDSU)
-FLDSU = os.environ.get("NLDPC_GEN_FLDSU", "0") == "1"
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
 # chosen by auto_geometry
@@ -931,17 +929,11 @@ def emit(S: Spec) -> str:
     w(f"    const uint32_t vc = g < nlive && !dup_ ? 4u * (g * {S.E * Z} + u) : 0x80000000u;  // [E][Z] c2v state")
     w(f"    const rsrc_t xr = make_rsrc(a.xa + blk * {NZ}, nlive * {4 * NZ});")
     w(f"    const rsrc_t cr = make_rsrc(a.c2v_out ? a.c2v_out + blk * {S.E * Z} : a.xa, nlive * {4 * S.E * Z});")
-    if S.uremat and FLDSU:  # (one unpadded codeword per workgroup: g is 0 and wave-uniform)
-        w(f"    float* lds = lds_all + __builtin_amdgcn_readfirstlane(g) * {S.cw_floats};")
-    else:
-        w(f"    float* lds = lds_all + (dup_ ? {G} : g) * {S.cw_floats};  // (repeating lanes: their own region)")
+    w(f"    float* lds = lds_all + (dup_ ? {G} : g) * {S.cw_floats};  // (repeating lanes: their own region)")
     w("    const uint32_t vm = vo >> 2;  // byte offsets of the uint8 clamp masks")
     w(f"    __shared__ int cnt_all[{G * 32}];  // count-only decode: per codeword, two iterations per word")
     w(f"    __shared__ uint32_t app_all[{S.G_lds * S.N * S.WZX}];  // UCN: bit (j, v) = APP[j][v] >= 0, per codeword")
-    if S.uremat and FLDSU:
-        w(f"    uint32_t* appw = app_all + __builtin_amdgcn_readfirstlane(g) * {S.N * S.WZX};")
-    else:
-        w(f"    uint32_t* appw = app_all + (dup_ ? {G} : g) * {S.N * S.WZX};")
+    w(f"    uint32_t* appw = app_all + (dup_ ? {G} : g) * {S.N * S.WZX};")
     w(f"    if constexpr (CNT) {{ for (int i = t; i < {G * 32}; i += {S.threads}) cnt_all[i] = 0; }}  // first use after iteration 0's barriers")
     if S.uremat:
         w("    const int ub = __builtin_amdgcn_readfirstlane(u - lane_id());  // (UREMAT) u of the wave's lane 0")
