@@ -1223,19 +1223,23 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 nb = (e1c - e0c) * Z * SBY
                 W_ = S.stage_width
                 w("template <int KIND>")
+                # r5: 32-bit offsets into a descriptor over the block's chunk instead of 64-bit lane addresses,
+                # the lane from v_mbcnt and the wave's first thread index (w0, wave-uniform) from the caller --
+                # none of them kept live across the iteration (the tied kernel had spilled them and reloaded
+                # them every phase: spilled VGPRs 21 -> 4, cfg5 backward 26.3 -> 25.0 ms, profiles/r5u_*)
                 w(f"__device__ __forceinline__ void stage_c{ci}(const FusedBwdArgs& a, int it, int64_t blk, int nlive, "
-                  "char* stg_all) {")
-                w(f"    const int t = threadIdx.x, lane = t & 63, w0 = t & ~63;")
+                  "char* stg_all, int w0) {")
                 w(f"    constexpr int NP = {nb // W_};  // {W_}-byte pieces")
+                w("    const int lane = lane_id();")
                 w(f"    const char* src = a.sv2c + ((int64_t)it * a.sv2c_stride + blk * {E * Z}) * {SBY} + {e0c * Z * SBY};")
                 w("#pragma unroll")
                 w(f"    for (int g = 0; g < {G}; ++g) {{")
                 w("        if (g >= nlive) break;")
-                w(f"        const char* sg = src + (int64_t)g * {E * Z * SBY};")
+                w(f"        const rsrc_t sr = make_rsrc((const float*)(src + (int64_t)g * {E * Z * SBY}), {nb});")
                 w(f"        char* dg = stg_all + g * {4 * S.stage_floats};")
                 w(f"        for (int i = w0; i < NP; i += {S.threads}) {{")
-                w(f"            if (i + lane < NP) __builtin_amdgcn_global_load_lds((gptr_t)(sg + (int64_t)(i + lane) * {W_}), "
-                  f"(lptr_t)(dg + i * {W_}), {W_}, 0, 0);")
+                w(f"            if (i + lane < NP) __builtin_amdgcn_raw_ptr_buffer_load_lds(sr, (lptr_t)(dg + i * {W_}), {W_}, "
+                  f"(uint32_t)(i + lane) * {W_}u, 0, 0, 0);")
                 w("        }")
                 w("    }")
                 w("}")
@@ -1246,7 +1250,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w("template <int KIND, int TIED>")
         w(f"__device__ __forceinline__ void bwd_p{p}(const FusedBwdArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"uint32_t vo, uint32_t vm, uint32_t vcw, int slot, bool lane0, bool dup_, const char* stg, char* stg_all, "
-          f"float* gacc) {{")
+          f"float* gacc, int wb) {{")
         for q in range(Q):
             w(f"    float g{q}[{sp}];")
         w(f"    const rsrc_t cyr = make_rsrc(a.carry ? a.carry + blk * {NZ} : nullptr, a.carry ? nlive * {4 * NZ} : 0);")
@@ -1293,7 +1297,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         bstamp(0)
         for ci in range(len(S.chunks)):
             if SBY:  # the chunk's saved messages start moving into LDS now and land by the barrier
-                w(f"        stage_c{ci}<KIND>(a, it, blk, nlive, stg_all);")
+                w(f"        stage_c{ci}<KIND>(a, it, blk, nlive, stg_all, wb);")
             w(f"        wrb_p{p}_c{ci}<KIND>({state_args()}, lds, u, gr, mr, vo, vm);")
             bstamp(1 + 3 * ci)
             if SBY:
@@ -1348,6 +1352,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     w(f"    const uint32_t vcw = g < nlive && !dup_ ? 4u * (g * {E * Z}) : 0x80000000u;  // codeword base in [E][Z] (CN gathers)")
     w("    const int slot = blockIdx.x * WP + __builtin_amdgcn_readfirstlane(r0_ >> 6);")
     w("    const bool lane0 = (t & 63) == 0;")
+    w("    const int wb = __builtin_amdgcn_readfirstlane(t) & ~63;  // the wave's first thread index (staging)")
     if not S.padded and ZT % 64 == 0:
         # every wave lies in one codeword: its LDS regions are wave-uniform (scalar bases, nothing per lane to keep)
         w(f"    const int gw_ = __builtin_amdgcn_readfirstlane(g);")
@@ -1360,7 +1365,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w(f"    for (int i = t; i < {STF}; i += {S.threads}) ((float*)(stg_all + {G * 4 * STF}))[i] = 0.f;")
     for p in range(S.P):
         w(f"    {'if' if p == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND, TIED>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0, dup_, "
-          "stg, stg_all, gacc);")
+          "stg, stg_all, gacc, wb);")
     w("}")
     # a tied CN weight (cfg5's NW(3,0,3): one CN weight per iteration): a separate kernel (TIED = 1) reduces
     # each row copy's contributions once (one wave reduction per row copy into the wave's LDS sum) instead of
