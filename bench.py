@@ -6,7 +6,9 @@
 
 Default workload cfg3: a step = one NeuralLDPCDecoder.forward over the rank's batch of B codewords
 (default 65536 per GPU, weak scaling), T=20 iterations, every iteration's posterior written (the
-reference API's output list).  cfg2: the same on WiMAX N=576 R=3/4 z=24, B=4096.  cfg5: one
+reference API's output list).  At N=1 the default run also times the other single-GPU BASELINE configs
+with the same timed() helper and reports them under `side_lines` (never as `value`): cfg5 and cfg2
+(--no-side-lines skips them).  cfg2: the same decode on WiMAX N=576 R=3/4 z=24, B=4096.  cfg5: one
 BoostedNeuralLDPCDecoder training step (QMS q=5, NW(3,0,3), T=50, B=2048: forward over all
 iterations, LDPCDecoderLoss BCE, backward, clip_grad_norm 1.0, Adam, weight clamp), as
 train/train_BoostedNeuralLDPCDecoder.py:278-294 does it.
@@ -72,6 +74,8 @@ def parse():
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="decode steps as replays of one captured HIP graph (auto: cfg2, whose 0.1 ms kernel is "
                          "comparable to the host path of a module call)")
+    ap.add_argument("--no-side-lines", action="store_true", help="default cfg3 run at N=1: skip the cfg5 / cfg2 lines")
+    ap.add_argument("--side-steps-cfg2", type=int, default=200, help="timed steps of the cfg2 side line")
     ap.add_argument("--nw", default="1,1,2", help="cfg3ucn: NodeWeightSharingConfig (cn, ucn, vn) codes")
     ap.add_argument("--kind", default="MS", choices=("MS", "QMS", "SP"), help="cfg3ucn: Boosted decoding type")
     return ap.parse_args()
@@ -158,13 +162,15 @@ def pmc_workload(args):
     return args.workload
 
 
-def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings, pmc_key, T=None):
+def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings, pmc_key, T=None, cus=256):
     """Roofline of the dominant kernel: the algorithmic bytes it must move per launch over its average
     HIP-event launch time, against the 8 TB/s HBM spec (and the measured HBM ceilings); HBM traffic
     and VALU issue from the committed PMC summary of the same workload when present.  `frac` is always
     the compulsory-byte HBM fraction (the north star's quote); `bound` names the ceiling the evidence says
     binds: "valu" when the committed ISA budget's issue floor (profiles/isa_budget.json at the PMC effective
-    clock) is a larger fraction of the launch than the bytes are of HBM peak, else "hbm"."""
+    clock) is at least half of the launch and a larger fraction than the bytes are of HBM peak; "hbm" when the
+    bytes reach half of the HBM peak; "latency" when neither does and the PMC says the waves mostly wait
+    (SQ_WAIT_ANY); "unknown" when no evidence names a ceiling (never "hbm" by default)."""
     per = {}
     for k in KINDS:
         ms_tot, n = prof[k]
@@ -177,7 +183,7 @@ def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings,
     pmc = load_pmc(f"{dom}_{pmc_key}")
     traffic = pmc.get("bytes") if pmc else None
     kname = KERNEL_NAMES[dom].replace("<graph>", graph_tag)
-    r = {"bound": "hbm", "kernel": kname,
+    r = {"bound": "unknown", "kernel": kname,
          "achieved": round(d["gbs"], 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
          "frac": round(d["gbs"] / PEAK_HBM_GBS, 4), "traffic": traffic,
          "alg_bytes_per_launch": d["alg_bytes_per_launch"], "avg_launch_ms": round(d["avg_ms"], 4),
@@ -205,29 +211,36 @@ def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings,
                                                     "(1024 SIMDs x effective clock x launch time): pmc.valu_mix")
     # the issue floor of the instruction stream (ISA budget), at the clock the PMC pass measured
     budget = load_isa_budget(pmc.get("kernel") if pmc and pmc.get("kernel") else kname)
-    if budget and T:
+    if budget and T and budget.get("G"):  # (an entry without its geometry's G is not used: ADVICE r5)
         clk = (pmc.get("effective_clock_ghz") if pmc else None) or budget.get("clock_ghz", 2.4)
-        G = budget.get("G", 1)  # codewords per workgroup of the budgeted geometry
-        wg_iters_per_cu = -(-B // G) / 256.0 * T  # workgroup-iterations per CU (one workgroup per CU at a time)
+        G = budget["G"]  # codewords per workgroup of the budgeted geometry
+        # workgroup-iterations per CU; the budget is the busiest SIMD's issue cycles per workgroup-iteration (with
+        # several workgroups per CU its waves' total over the 4 SIMDs: tools/isa_budget.py)
+        wg_iters_per_cu = -(-B // G) / float(cus) * T
         floor_ms = budget["simd_issue_cycles_per_wg_iter"] * wg_iters_per_cu / (clk * 1e9) * 1e3
         r["issue_floor_ms"] = round(floor_ms, 3)
         r["issue_frac"] = round(floor_ms / d["avg_ms"], 4)
         r["issue_floor"] = {"simd_issue_cycles_per_wg_iter": budget["simd_issue_cycles_per_wg_iter"],
-                            "clock_ghz": round(clk, 4), "wg_iters_per_cu": wg_iters_per_cu,
+                            "clock_ghz": round(clk, 4), "wg_iters_per_cu": wg_iters_per_cu, "cus": cus,
                             "source": budget.get("source"),
                             "note": "VALU issue cycles of the busier SIMD set per workgroup-iteration (ISA of the "
                                     "hot loop at the measured per-class issue costs) x workgroup-iterations per CU / "
                                     "PMC effective clock: the launch time with no stall at all"}
-        if r["issue_frac"] > r["frac"]:
-            r["bound"] = "valu"
-    # neither ceiling near: the waves mostly wait (PMC SQ_WAIT_ANY over wave-cycles) -- a latency-bound kernel
-    # (the cfg5 backward: LDS round trips and barriers)
-    valu_frac = r.get("valu_issue", {}).get("weighted_frac_of_simd_cycles") or r.get("valu_issue", {}).get("frac_of_peak")
+    # the label: the ceiling the evidence puts nearest (the ISA issue floor or the PMC-weighted VALU issue, the
+    # compulsory HBM bytes), a latency-bound kernel when neither is near and the waves mostly wait (PMC SQ_WAIT_ANY
+    # over wave-cycles: the cfg5 backward's LDS round trips and barriers), else "unknown"
+    valu_frac = r.get("issue_frac") or r.get("valu_issue", {}).get("weighted_frac_of_simd_cycles")
     wait = pmc.get("wait_any_over_wave_cycles") if pmc else None
-    if r["bound"] == "hbm" and wait is not None and wait >= 0.5 and r["frac"] < 0.5 and (valu_frac or 0) < 0.5:
+    if valu_frac is not None and valu_frac >= 0.5 and valu_frac > r["frac"]:
+        r["bound"] = "valu"
+    elif r["frac"] >= 0.5:
+        r["bound"] = "hbm"
+    elif wait is not None and wait >= 0.5:
         r["bound"] = "latency"
-        r["bound_evidence"] = (f"HBM {r['frac']:.2f} of peak, VALU issue {valu_frac or 0:.2f} of peak, "
-                               f"SQ_WAIT_ANY / wave-cycles {wait:.2f} (PMC)")
+    r["bound_evidence"] = (f"HBM {r['frac']:.2f} of peak (compulsory bytes); VALU issue "
+                           f"{'%.2f' % valu_frac if valu_frac is not None else 'unmeasured'} of the launch "
+                           f"({'ISA issue floor' if r.get('issue_frac') else 'PMC class-weighted' if valu_frac is not None else 'no ISA budget / PMC'}); "
+                           f"SQ_WAIT_ANY / wave-cycles {'%.2f' % wait if wait is not None else 'unmeasured'}")
     if dom == "fused" and d5_bytes_per_cw:
         # SURVEY §8(d) D5 models a flooding decoder whose E*Z message state crosses HBM every iteration;
         # the fused kernel keeps that state on chip, so this is an equivalent rate, not traffic
@@ -287,6 +300,43 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def run_workload(args, rank, world, local, dev, cus, ceilings):
+    """One workload's line (args.workload, with its default batch / iterations unless given)."""
+    gfile, Z, T, B = WORKLOADS[args.workload]
+    T = args.iters or T
+    B = args.batch or B
+    bg = np.loadtxt(os.path.join(ROOT, "resources", gfile), int, delimiter="\t")
+    if args.workload == "cfg5":
+        return bench_train(args, rank, world, local, dev, bg, Z, T, B, cus, ceilings)
+    return bench_decode(args, rank, world, local, dev, bg, Z, T, B, cus, ceilings)
+
+
+# what a side line keeps of its workload's own line
+SIDE_KEYS = ("value", "unit", "ms_per_step", "ms_per_step_median", "value_from_median", "steps", "warmup", "timing",
+             "dtype", "config", "loss", "ber", "roofline")
+
+
+def side_lines(args, rank, world, local, dev, cus, ceilings):
+    """the default N=1 run also times every other single-GPU BASELINE config with the same
+    timed() helper -- cfg5 (BASELINE configs[4]: the Boosted training step, forward + BCE + backward + Adam) and
+    cfg2 (configs[1]: WiMAX z=24, B=4096, HIP-graph replay with the eager timing beside) -- each at its own default
+    batch and iterations.  Reported under `side_lines`, never as `value`."""
+    import copy
+    out = {}
+    for wl, steps, warmup in (("cfg5", args.steps, args.warmup), ("cfg2", args.side_steps_cfg2, 20)):
+        a = copy.copy(args)
+        a.workload, a.steps, a.warmup = wl, steps, warmup
+        a.batch = a.iters = None
+        a.no_sweep = a.no_count_only = a.no_cpu_baseline = True
+        a.graph = "auto"
+        torch.cuda.empty_cache()
+        r = run_workload(a, rank, world, local, dev, cus, ceilings)
+        if rank == 0:
+            out[wl] = {k: r[k] for k in SIDE_KEYS if k in r}
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     rc = launch_ranks(args)
@@ -298,14 +348,15 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but {world} rank(s) are running")
     dev = torch.device("cuda", local if args.backend == "nccl" else local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    gfile, Z, T, B = WORKLOADS[args.workload]
-    T = args.iters or T
-    B = args.batch or B
-    bg = np.loadtxt(os.path.join(ROOT, "resources", gfile), int, delimiter="\t")
-    if args.workload == "cfg5":
-        res = bench_train(args, rank, world, local, dev, bg, Z, T, B)
-    else:
-        res = bench_decode(args, rank, world, local, dev, bg, Z, T, B)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count  # (not a hard-coded 256)
+    # measured HBM ceilings, once, before any workload allocates
+    ceilings = hbm_ceilings(dev) if (rank == 0 and not args.no_profile) else None
+    res = run_workload(args, rank, world, local, dev, cus, ceilings)
+    if (args.workload == "cfg3" and world == 1 and not args.no_side_lines and args.batch is None
+            and args.iters is None):
+        side = side_lines(args, rank, world, local, dev, cus, ceilings)
+        if rank == 0:
+            res["side_lines"] = side
     if rank == 0:
         print(json.dumps(res), flush=True)
     nd_dist.barrier(local)
@@ -335,7 +386,7 @@ def timed(args, local, dev, step, prof):
     return elapsed, prof.end(), step_ms
 
 
-def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
+def bench_decode(args, rank, world, local, dev, bg, Z, T, B, cus=256, ceilings=None):
     import neural_ldpc_decoder as nd
     from nldpc import distributed as nd_dist
     from nldpc.channel import awgn_llr, ber_counts, sigma_for
@@ -426,7 +477,6 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
                 sweep["bit_errors"].append(int(c[-1, 0]))
                 sweep["frame_errors"].append(int(c[-1, 1]))
                 del x
-    ceilings = hbm_ceilings(dev) if (rank == 0 and not args.no_profile) else None
     elapsed = nd_dist.max_time(elapsed, device=dev)
     med = nd_dist.max_time(statistics.median(step_ms) / 1000.0, device=dev)
     counts = nd_dist.sum_counts(counts).cpu().numpy()  # the one RCCL exchange: BER accounting
@@ -448,6 +498,9 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
         "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
         "ms_per_step_median": round(1000.0 * med, 3),
         "value_from_median": round(world * B / med, 1),
+        # the timing mode of ms_per_step / value (cfg2's auto mode replays a captured HIP graph; its eager
+        # module-call timing stays in config.graph.eager)
+        "timing": "graph_replay" if graph_info else "eager",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -478,13 +531,13 @@ def bench_decode(args, rank, world, local, dev, bg, Z, T, B):
     if prof is not None:
         res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T), args.steps, B, Z, world, tag,
                                    4 * (2 * T * E * Z + (T + 1) * N * Z), ceilings, pmc_workload(args) + f"_B{B}",
-                                   T=T)
+                                   T=T, cus=cus)
     if world == 1 and not args.no_cpu_baseline and not ucn:
         res["cpu_baseline"] = cpu_baseline(bg, Z, T, xa_host, gpu_last, args.cpu_seconds)
     return res
 
 
-def bench_train(args, rank, world, local, dev, bg, Z, T, B):
+def bench_train(args, rank, world, local, dev, bg, Z, T, B, cus=256, ceilings=None):
     """cfg5: one training step of BoostedNeuralLDPCDecoder per step (train_BoostedNeuralLDPCDecoder.py:278-294)."""
     from boosted_neural_ldpc_decoder.BoostedNeuralLDPCDecoder import BoostedNeuralLDPCDecoder
     from boosted_neural_ldpc_decoder.ConnectingMatrix import ConnectingMatrix
@@ -537,6 +590,7 @@ def bench_train(args, rank, world, local, dev, bg, Z, T, B):
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
         "ms_per_step_median": round(1000.0 * med, 3),
+        "timing": "eager",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -553,7 +607,7 @@ def bench_train(args, rank, world, local, dev, bg, Z, T, B):
     }
     if prof is not None:
         res["roofline"] = roofline(prof, kernel_bytes(B, E, N, Z, T, train={"qms": True, "vn": True}), args.steps, B, Z,
-                                   world, "bg2_z384", None, None, f"{args.workload}_B{B}")
+                                   world, "bg2_z384", None, ceilings, f"{args.workload}_B{B}", T=T, cus=cus)
     return res
 
 

@@ -68,7 +68,10 @@ typedef struct nldpc_cfg {
 #define NLDPC_FLAG_CN_TIED 8     /* (ABI 4, nldpc_backward) every row of w_cn repeats one weight (sharing code 3,
                                     BoostedNeuralLDPCDecoder.py:114-124): g_w_cn may receive each iteration's total
                                     in a few entries of its row and zeros elsewhere -- only row sums are meaningful,
-                                    which is all a tied weight's gradient is */
+                                    which is all a tied weight's gradient is.  The results (every gradient) are
+                                    UNDEFINED unless every row of w_cn is one value: the tied kernel derives a row's
+                                    check-node masks from its first weight (the Python side sets the flag only for a
+                                    stride-0 expand, nldpc.decode._honour_tied) */
 
 /* ---- library ---------------------------------------------------------------------------- */
 int nldpc_abi_version(void);
@@ -95,9 +98,17 @@ int nldpc_graph_edges(const nldpc_graph* g, int32_t* chk, int32_t* var, int32_t*
  *      it is what makes ConnectingMatrix(Z, basegraph) at any Z (ConnectingMatrix.py:5-53) fast.
  *      The code object's global nldpc_sig (the kernel argument layout it was generated for) must be this
  *      library's, else NLDPC_EUNSUPPORTED (r5: a skewed build is refused instead of running a kernel that
- *      leaves its outputs unwritten). */
+ *      leaves its outputs unwritten).  r6: the signature is read from the host copy of the code object (no
+ *      device copy, no wait on work in flight).  Loading the module (hipModuleLoadData) is not a stream
+ *      operation: attach a geometry's kernels -- i.e. run the first decode of a run-time geometry -- outside
+ *      any stream / graph capture (nldpc.jit compiles and attaches on that first call). */
 int nldpc_graph_attach_kernel(nldpc_graph* g, int32_t mode, int32_t kind, const void* code, size_t bytes,
                               int32_t G, int32_t threads, int32_t waves_per_part);
+/* (r6, additive to ABI 4) The argument-layout signature a code object was generated for (its nldpc_sig, read on the host from
+ *      the hipcc --genco offload bundle or a bare gfx950 ELF) and the one this library's mode needs (mode 0-3:
+ *      forward kernels, 4: backward).  NLDPC_EINVAL when the object carries no readable nldpc_sig.  Lets a
+ *      caller validate a cached code object before nldpc_graph_attach_kernel; no device is touched. */
+int nldpc_code_object_sig(const void* code, size_t bytes, int32_t mode, uint32_t* sig, uint32_t* expected);
 /* (ABI 3) *mask: bit (mode * 4 + kind) set when that fused kernel exists for the graph (modes as above) */
 int nldpc_graph_kernels(const nldpc_graph* g, uint32_t* mask);
 
@@ -238,7 +249,8 @@ int nldpc_profile_end(int32_t nkinds, float* ms, int32_t* count);
 /* ---- benchmark instrumentation: measured HBM ceilings (SURVEY §8(d) D4 "report the measured
  *   stream-copy ceiling too").  One launch over n floats (n % 4 == 0; 16 B per lane unless stated):
  *   kind 0 = copy src -> dst, 1 = write-only fill of dst, 2 = read-only pass over src (dst receives
- *   one float4 per workgroup, 8192 workgroups), 3 = read-only with 4 B per lane (dst as for 2). */
+ *   one float4 per workgroup, 2048 workgroups), 3 = read-only with 4 B per lane (dst receives one float4 per
+ *   workgroup, 8192 workgroups).  r6: kinds 0-2 keep 8 float4 loads in flight per lane, non-temporal. */
 int nldpc_hbm_probe(int32_t kind, float* dst, const float* src, int64_t n, void* stream);
 
 #ifdef __cplusplus

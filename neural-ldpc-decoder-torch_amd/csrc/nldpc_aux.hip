@@ -256,38 +256,60 @@ __global__ __launch_bounds__(256) void bce_grad_kernel(BceArgs a, const float* _
 }
 
 // ---------------------------------------------------------------- HBM ceiling probes (bench.py roofline)
-// 16 B per lane, grid-stride, enough workgroups to cover every CU many times over.  kind 0: stream
-// copy (read + write), 1: write-only fill (the decoder's traffic is ~95 % posterior writes), 2: read
-// only (one partial sum per workgroup is written so the loads are live), 3: read only with 4 B per
-// lane, the decoder's own load width (calibrates the FETCH_SIZE counter for those loads).
-__global__ __launch_bounds__(256) void hbm_probe_kernel(int kind, float4* __restrict__ dst,
-                                                        const float4* __restrict__ src, int64_t n4) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (kind == 0) {
-        for (; i < n4; i += stride) dst[i] = src[i];
-    } else if (kind == 1) {
-        const float4 v = make_float4(1.f, 2.f, 3.f, 4.f);
-        for (; i < n4; i += stride) dst[i] = v;
-    } else {
-        float acc = 0.f;
-        if (kind == 2) {
-            for (; i < n4; i += stride) {
-                const float4 v = src[i];
-                acc += (v.x + v.y) + (v.z + v.w);
+// kind 0: stream copy (read + write), 1: write-only fill (the decoder's traffic is ~95 % posterior writes), 2: read
+// only (one partial sum per workgroup is written so the loads are live): 16 B per lane, each workgroup moving tiles of
+// 256 lanes x kUnroll float4 (every load of a tile issued before its first use, 8 loads in flight per lane;
+// non-temporal, as the decoder's posterior stores), grid-stride over the tiles.  VERDICT r5: the r5 probe (one float4
+// per lane and trip) measured copy 4.8 TB/s against the guide's 6.29 TB/s float4 copy.  kind 3: read only with 4 B
+// per lane, the decoder's own load width (calibrates the FETCH_SIZE counter for those loads; kept as it was).
+constexpr int kProbeUnroll = 8;
+typedef float probe_v4 __attribute__((ext_vector_type(4)));  // (the nontemporal builtins take native vectors)
+__global__ __launch_bounds__(256) void hbm_probe_kernel(int kind, float4* __restrict__ dst4,
+                                                        const float4* __restrict__ src4, int64_t n4) {
+    constexpr int64_t TILE = 256 * kProbeUnroll;
+    probe_v4* dst = reinterpret_cast<probe_v4*>(dst4);
+    const probe_v4* src = reinterpret_cast<const probe_v4*>(src4);
+    const int64_t ntiles = n4 / TILE;
+    float acc = 0.f;
+    if (kind <= 2) {
+        for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+            const int64_t base = t * TILE + threadIdx.x;
+            if (kind == 1) {
+                const probe_v4 v = {1.f, 2.f, 3.f, 4.f};
+#pragma unroll
+                for (int k = 0; k < kProbeUnroll; ++k) __builtin_nontemporal_store(v, dst + base + k * 256);
+                continue;
             }
-        } else {
-            const float* s1 = reinterpret_cast<const float*>(src);
-            for (; i < 4 * n4; i += stride) acc += s1[i];
+            probe_v4 v[kProbeUnroll];
+#pragma unroll
+            for (int k = 0; k < kProbeUnroll; ++k) v[k] = __builtin_nontemporal_load(src + base + k * 256);
+            if (kind == 0) {
+#pragma unroll
+                for (int k = 0; k < kProbeUnroll; ++k) __builtin_nontemporal_store(v[k], dst + base + k * 256);
+            } else {
+#pragma unroll
+                for (int k = 0; k < kProbeUnroll; ++k) acc += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+            }
         }
-        __shared__ float red[256];
-        red[threadIdx.x] = acc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            float s = 0.f;
-            for (int k = 0; k < 256; ++k) s += red[k];
-            dst[blockIdx.x] = make_float4(s, 0.f, 0.f, 0.f);
+        // the tail past the last whole tile (n4 % TILE float4), one float4 per lane
+        for (int64_t i = ntiles * TILE + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+            if (kind == 0) dst[i] = src[i];
+            else if (kind == 1) dst[i] = probe_v4{1.f, 2.f, 3.f, 4.f};
+            else acc += (src[i].x + src[i].y) + (src[i].z + src[i].w);
         }
+        if (kind != 2) return;
+    } else {
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        const float* s1 = reinterpret_cast<const float*>(src4);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 4 * n4; i += stride) acc += s1[i];
+    }
+    __shared__ float red[256];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int k = 0; k < 256; ++k) s += red[k];
+        dst4[blockIdx.x] = make_float4(s, 0.f, 0.f, 0.f);
     }
 }
 
@@ -299,7 +321,8 @@ extern "C" int nldpc_hbm_probe(int32_t kind, float* dst, const float* src, int64
     if (kind < 0 || kind > 3 || !dst || (kind != 1 && !src) || n <= 0 || (n & 3))
         return fail(NLDPC_EINVAL, "nldpc_hbm_probe: bad argument");
     const int64_t n4 = n >> 2;
-    const int blocks = 256 * 32;  // 32 workgroups of 256 per CU
+    // kinds 0-2: 8 workgroups of 256 per CU, each looping over 32 KB tiles; kind 3: 32 per CU (the r2 calibration)
+    const int blocks = kind == 3 ? 256 * 32 : 256 * 8;
     hipLaunchKernelGGL(hbm_probe_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), kind,
                        reinterpret_cast<float4*>(dst), reinterpret_cast<const float4*>(src), n4);
     hipError_t e = hipGetLastError();

@@ -271,6 +271,87 @@ FusedLaunch fused_launch(const nldpc_graph* g, int mode, int kind) {
 }
 }  // namespace nldpc
 
+namespace {
+// The initial value of the code object's global `nldpc_sig` (gen_fused.py jit_source), read from the host copy
+// of the code object: a clang offload bundle (hipcc --genco) holding the gfx950 ELF, or the ELF itself.  No device
+// copy, so the check neither waits for work in flight nor touches a stream that may be capturing.
+bool code_object_sig(const void* code, size_t bytes, uint32_t* sig) {
+    const auto* b = static_cast<const unsigned char*>(code);
+    auto rd64 = [&](size_t off, uint64_t* v) {
+        if (off > bytes || bytes - off < 8) return false;
+        std::memcpy(v, b + off, 8);
+        return true;
+    };
+    static const char kBundle[] = "__CLANG_OFFLOAD_BUNDLE__";
+    const unsigned char* elf = b;
+    size_t elf_bytes = bytes;
+    if (bytes >= 24 && std::memcmp(b, kBundle, 24) == 0) {
+        uint64_t n = 0, pos = 24;
+        if (!rd64(pos, &n)) return false;
+        pos += 8;
+        elf = nullptr;
+        for (uint64_t i = 0; i < n && i < 64; ++i) {
+            uint64_t off, sz, tl;
+            if (!rd64(pos, &off) || !rd64(pos + 8, &sz) || !rd64(pos + 16, &tl)) return false;
+            pos += 24;
+            if (pos > bytes || tl > bytes - pos) return false;
+            const std::string triple(reinterpret_cast<const char*>(b + pos), tl);
+            pos += tl;
+            if (triple.find("amdgcn") != std::string::npos && off <= bytes && sz <= bytes - off && sz >= 64) {
+                elf = b + off;
+                elf_bytes = sz;
+                break;
+            }
+        }
+        if (!elf) return false;
+    }
+    // ELF64 little endian: the symbol table, the symbol, the initialised bytes of its section
+    if (elf_bytes < 64 || std::memcmp(elf, "\x7f" "ELF", 4) != 0 || elf[4] != 2 || elf[5] != 1) return false;
+    auto u16 = [&](size_t o) { uint16_t v; std::memcpy(&v, elf + o, 2); return (size_t)v; };
+    auto u32 = [&](size_t o) { uint32_t v; std::memcpy(&v, elf + o, 4); return (size_t)v; };
+    auto u64 = [&](size_t o) { uint64_t v; std::memcpy(&v, elf + o, 8); return (size_t)v; };
+    const size_t shoff = u64(0x28), shentsize = u16(0x3a), shnum = u16(0x3c);
+    if (shentsize < 64 || shoff > elf_bytes || shnum > (elf_bytes - shoff) / shentsize) return false;
+    auto sh = [&](size_t i, size_t field) { return shoff + i * shentsize + field; };
+    for (size_t s = 0; s < shnum; ++s) {
+        if (u32(sh(s, 4)) != 2 /* SHT_SYMTAB */ && u32(sh(s, 4)) != 11 /* SHT_DYNSYM */) continue;
+        const size_t off = u64(sh(s, 0x18)), size = u64(sh(s, 0x20)), link = u32(sh(s, 0x28)),
+                     ent = u64(sh(s, 0x38));
+        if (ent < 24 || link >= shnum || off > elf_bytes || size > elf_bytes - off) return false;
+        const size_t stroff = u64(sh(link, 0x18)), strsize = u64(sh(link, 0x20));
+        if (stroff > elf_bytes || strsize > elf_bytes - stroff) return false;
+        for (size_t k = 0; k < size / ent; ++k) {
+            const size_t sym = off + k * ent, name = u32(sym);
+            if (name >= strsize) continue;
+            const char* nm = reinterpret_cast<const char*>(elf + stroff + name);
+            if (strnlen(nm, strsize - name) != 9 || std::memcmp(nm, "nldpc_sig", 9) != 0) continue;
+            const size_t shndx = u16(sym + 6), value = u64(sym + 8), symsize = u64(sym + 16);
+            if (symsize != 4 || shndx == 0 || shndx >= shnum) return false;
+            if (u32(sh(shndx, 4)) == 8 /* SHT_NOBITS */) {
+                *sig = 0;
+                return true;
+            }
+            const size_t saddr = u64(sh(shndx, 0x10)), soff = u64(sh(shndx, 0x18)), ssize = u64(sh(shndx, 0x20));
+            if (value < saddr || value - saddr > ssize || ssize - (value - saddr) < 4) return false;
+            const size_t at = soff + (value - saddr);
+            if (at > elf_bytes || elf_bytes - at < 4) return false;
+            std::memcpy(sig, elf + at, 4);
+            return true;
+        }
+    }
+    return false;
+}
+}  // namespace
+
+extern "C" int nldpc_code_object_sig(const void* code, size_t bytes, int32_t mode, uint32_t* sig, uint32_t* expected) {
+    if (!code || !bytes || !sig || !expected || mode < 0 || mode > 4)
+        return fail(NLDPC_EINVAL, "nldpc_code_object_sig: null argument or mode outside 0-4");
+    *expected = mode == 4 ? kFusedBwdArgsSig : kFusedArgsSig;
+    if (!code_object_sig(code, bytes, sig))
+        return fail(NLDPC_EINVAL, "nldpc_code_object_sig: no readable nldpc_sig in the code object");
+    return NLDPC_OK;
+}
+
 extern "C" int nldpc_graph_attach_kernel(nldpc_graph* g, int32_t mode, int32_t kind, const void* code, size_t bytes,
                                          int32_t G, int32_t threads, int32_t waves_per_part) {
     if (!g || !code || !bytes) return fail(NLDPC_EINVAL, "nldpc_graph_attach_kernel: null argument");
@@ -285,22 +366,16 @@ extern "C" int nldpc_graph_attach_kernel(nldpc_graph* g, int32_t mode, int32_t k
     if (!first && (G != g->jit_G || threads != g->jit_threads || waves_per_part != g->jit_wpp))
         return fail(NLDPC_EINVAL, "nldpc_graph_attach_kernel: geometry differs from the graph's attached kernels");
     if (g->jit_fn[mode][kind]) return NLDPC_OK;
+    {  // the code object's argument layout (gen_fused.py jit_source: nldpc_sig) must be this library's
+        uint32_t sig = 0;
+        if (!code_object_sig(code, bytes, &sig) || sig != (mode == 4 ? kFusedBwdArgsSig : kFusedArgsSig))
+            return fail(NLDPC_EUNSUPPORTED, "nldpc_graph_attach_kernel: the code object was built for another "
+                                            "kernel argument layout (regenerate it with this library's gen_fused.py)");
+    }
     DeviceGuard guard(g->device);
     hipModule_t mod = nullptr;
     NLDPC_HIP_CHECK(hipModuleLoadData(&mod, code));
     hipFunction_t fn = nullptr;
-    {  // the code object's argument layout (gen_fused.py jit_source: nldpc_sig) must be this library's
-        hipDeviceptr_t sp = nullptr;
-        size_t sb = 0;
-        uint32_t sig = 0;
-        if (hipModuleGetGlobal(&sp, &sb, mod, "nldpc_sig") != hipSuccess || sb != sizeof(sig) ||
-            hipMemcpyDtoH(&sig, sp, sizeof(sig)) != hipSuccess ||
-            sig != (mode == 4 ? kFusedBwdArgsSig : kFusedArgsSig)) {
-            (void)hipModuleUnload(mod);
-            return fail(NLDPC_EUNSUPPORTED, "nldpc_graph_attach_kernel: the code object was built for another "
-                                            "kernel argument layout (regenerate it with this library's gen_fused.py)");
-        }
-    }
     hipError_t e = hipModuleGetFunction(&fn, mod, mode == 4 ? "nldpc_fxb" : "nldpc_fx");
     if (e != hipSuccess) {
         (void)hipModuleUnload(mod);

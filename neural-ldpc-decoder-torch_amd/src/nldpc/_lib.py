@@ -29,11 +29,12 @@ EXPORTED = (
     "nldpc_graph_edges", "nldpc_graph_attach_kernel", "nldpc_graph_kernels", "nldpc_fast_path", "nldpc_saved_bytes", "nldpc_forward", "nldpc_backward_workspace", "nldpc_backward", "nldpc_ber_count",
     "nldpc_awgn_llr", "nldpc_profile_begin", "nldpc_profile_end", "nldpc_bce_workspace", "nldpc_bce_loss",
     "nldpc_bce_grad", "nldpc_bce_loss_grad", "nldpc_bce_grad_unless_unit", "nldpc_forward_count", "nldpc_channel_llr", "nldpc_hbm_probe",
+    "nldpc_code_object_sig",
 )
 
 
 # entries added after the ABI 4 structs were fixed (no layout change): optional in older builds
-_ADDED_IN_ABI4 = ("nldpc_bce_loss_grad", "nldpc_bce_grad_unless_unit")
+_ADDED_IN_ABI4 = ("nldpc_bce_loss_grad", "nldpc_bce_grad_unless_unit", "nldpc_code_object_sig")
 
 
 class NldpcCfg(ctypes.Structure):
@@ -78,6 +79,8 @@ def _declare(lib):
         "nldpc_graph_edges": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
         "nldpc_graph_attach_kernel": (_i32, [_vp, _i32, _i32, _vp, ctypes.c_size_t, _i32, _i32, _i32]),
         "nldpc_graph_kernels": (_i32, [_vp, ctypes.POINTER(ctypes.c_uint32)]),
+        "nldpc_code_object_sig": (_i32, [_vp, ctypes.c_size_t, _i32, ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.POINTER(ctypes.c_uint32)]),
         "nldpc_fast_path": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _i32, ctypes.POINTER(_i32)]),
         "nldpc_saved_bytes": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, ctypes.POINTER(ctypes.c_size_t)]),
         "nldpc_forward": (_i32, [_vp, ctypes.POINTER(NldpcCfg), _i64, _i32, _vp, _vp, _vp, _vp, _vp, _PP, _vp, _vp,

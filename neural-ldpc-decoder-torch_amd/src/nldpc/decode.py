@@ -141,6 +141,16 @@ def decode_count(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *
     return counts
 
 
+def _honour_tied(cfg: DecodeCfg, w_cn) -> DecodeCfg:
+    """cfg.cn_tied holds only for a w_cn whose rows are one repeated value by construction (an expand(): stride 0
+    along the edges, as the drop-in module passes sharing code 3); any other w_cn gets the per-edge gradient
+    (the tied kernel computes a row's masks from its first weight, so per-edge weights under the
+    flag would give wrong row sums)."""
+    if cfg.cn_tied and (w_cn is None or w_cn.dim() != 2 or w_cn.stride(1) != 0):
+        return dataclasses.replace(cfg, cn_tied=False)
+    return cfg
+
+
 def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, saved, *, w_cn=None, w_ucn=None,
                     bias=None, w_vn=None, app_prev=None, need=(True, True, True, True), c2v_in=False,
                     grad_state=None, want_state_grad=False):
@@ -149,6 +159,8 @@ def decode_backward(graph: LiftedGraph, cfg: DecodeCfg, xa, T, grad_outs, outs, 
     [B, E, Z] (None = zero).  Returns (g_w_cn, g_w_ucn, g_bias, g_w_vn, g_c2v_in)."""
     dev = xa.device
     B = int(xa.shape[0])
+    cfg = _honour_tied(cfg, w_cn)
+
     def z(ref, on):
         return torch.zeros(tuple(ref.shape), dtype=torch.float32, device=dev) if (ref is not None and on) else None
 
@@ -227,10 +239,7 @@ class DecodeFn(torch.autograd.Function):
 def decode_autograd(graph, cfg, xa, T, *, w_cn=None, w_ucn=None, bias=None, w_vn=None, c2v=None, app_prev=None):
     """Differentiable decode.  Returns (list of T outputs [B, N*Z], final state [B, E, Z]).  c2v: the
     incoming message state (None = all-zero); gradients flow into it when it requires grad.
-    cfg.cn_tied is honoured only for a w_cn whose rows are one repeated value by construction (an expand():
-    stride 0 along the edges, as the drop-in module passes sharing code 3); for any other w_cn the per-edge
-    gradient is computed (a tied backward on per-edge weights returns meaningless entries)."""
-    if cfg.cn_tied and (w_cn is None or w_cn.dim() != 2 or w_cn.stride(1) != 0):
-        cfg = dataclasses.replace(cfg, cn_tied=False)
+    cfg.cn_tied is honoured only for a stride-0 w_cn (_honour_tied)."""
+    cfg = _honour_tied(cfg, w_cn)
     res = DecodeFn.apply(graph, cfg, T, app_prev, xa, c2v, w_cn, w_ucn, bias, w_vn)
     return list(res[:T]), res[T]

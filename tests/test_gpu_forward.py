@@ -523,11 +523,13 @@ def test_tied_cn_backward_row_sums_match_untied(kind):
     if kind == 2:
         x = quantize(x, 5)
     x = x.to(DEV)
-    wc = (0.5 + torch.rand(T, 1, generator=gen)).expand(T, g.E).contiguous().to(DEV)
+    # (the tied flag is honoured for a stride-0 expand only, as the drop-in module passes code 3: decode._honour_tied)
+    wc1 = (0.5 + torch.rand(T, 1, generator=gen)).to(DEV)
     wv = (0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV)
     gy = [torch.randn(B, 52 * Z, generator=gen).to(DEV) for _ in range(T)]
     res = {}
     for tied in (False, True):
+        wc = wc1.expand(T, g.E) if tied else wc1.expand(T, g.E).contiguous()
         cfg = DecodeCfg(kind, qbit=5, vn_cumulative=True, path="fused", cn_tied=tied)
         outs, _, saved = decode(g, cfg, x, T, save=True, w_cn=wc, w_vn=wv)
         g_cn, _, _, g_vn, _ = decode_backward(g, cfg, x, T, gy, list(outs), saved, w_cn=wc, w_vn=wv)
@@ -536,6 +538,38 @@ def test_tied_cn_backward_row_sums_match_untied(kind):
     a, b = res[False][1].cpu().numpy(), res[True][1].cpu().numpy()
     np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-6 * np.abs(a).max())
     assert torch.equal(res[False][2], res[True][2])
+
+
+@pytest.mark.parametrize("kind", [1, 2])
+def test_tied_flag_on_per_edge_weights_gives_the_untied_gradient(kind):
+    """cn_tied=True with a per-edge (contiguous, non-uniform) w_cn must not reach the tied kernel (which
+    computes a row's masks from its first weight): decode_autograd and decode_backward both fall back to the per-edge
+    gradient, bit-identical to cn_tied=False."""
+    from nldpc.decode import DecodeCfg, decode, decode_autograd, decode_backward
+    from oracle.ldpc_oracle import quantize
+    T, B, Z = 4, 3, 16
+    g = _graph(BG2, Z)
+    gen = torch.Generator().manual_seed(40 + kind)
+    x = (2 * (-1 + 0.85 * torch.randn(B, 52, Z, generator=gen)) / 0.7225).float()
+    if kind == 2:
+        x = quantize(x, 5)
+    x = x.to(DEV)
+    wc = (0.5 + torch.rand(T, g.E, generator=gen)).to(DEV)  # per-edge: rows are NOT one value
+    wv = (0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV)
+    gy = [torch.randn(B, 52 * Z, generator=gen).to(DEV) for _ in range(T)]
+    res = {}
+    for tied in (False, True):
+        cfg = DecodeCfg(kind, qbit=5, vn_cumulative=True, path="fused", cn_tied=tied)
+        outs, _, saved = decode(g, cfg, x, T, save=True, w_cn=wc, w_vn=wv)
+        g_cn, _, _, g_vn, _ = decode_backward(g, cfg, x, T, gy, list(outs), saved, w_cn=wc, w_vn=wv)
+        a = wc.clone().requires_grad_(True)
+        v = wv.clone().requires_grad_(True)
+        ys, _ = decode_autograd(g, cfg, x, T, w_cn=a, w_vn=v)
+        torch.autograd.backward(ys, gy)
+        res[tied] = (g_cn, g_vn, a.grad, v.grad)
+    for u, t in zip(res[False], res[True]):
+        assert torch.equal(u, t)
+    assert torch.equal(res[True][0], res[True][2])
 
 
 @pytest.mark.parametrize("q", [0, 2])

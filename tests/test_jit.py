@@ -53,7 +53,38 @@ def test_jit_compiles_a_code_object(tmp_path, monkeypatch):
     assert b"nldpc_fx" in open(path, "rb").read()
     again, _ = jit.code_object(BG2, 52, 3, 0)  # a cache hit: same file, no recompile
     assert again == path
+    # the argument-layout signature is read from the host bytes (no device copy in attach)
+    import ctypes
+    from nldpc import _lib
+    L = _lib.lib()
+    data = open(path, "rb").read()
+    sig, exp = ctypes.c_uint32(), ctypes.c_uint32()
+    assert L.nldpc_code_object_sig(data, len(data), 0, ctypes.byref(sig), ctypes.byref(exp)) == _lib.NLDPC_OK
+    assert sig.value == exp.value != 0
+    assert L.nldpc_code_object_sig(data, len(data), 4, ctypes.byref(sig), ctypes.byref(exp)) == _lib.NLDPC_OK
+    assert sig.value != exp.value  # a forward kernel is not a backward one
+    assert L.nldpc_code_object_sig(data[:200], 200, 0, ctypes.byref(sig), ctypes.byref(exp)) == _lib.NLDPC_EINVAL
     shutil.rmtree(tmp_path, ignore_errors=True)
+
+
+def test_code_object_sig_reads_a_tampered_layout(tmp_path):
+    """A code object generated with another nldpc_sig value reads back that value (what
+    nldpc_graph_attach_kernel compares before loading the module)."""
+    import ctypes
+    import subprocess
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc not installed")
+    from nldpc import _lib, jit
+    src, _ = _gen().jit_source(BG2, 16, 3, 0)
+    bad = src.replace("nldpc_sig = nldpc::kFusedArgsSig", "nldpc_sig = 0x12345678u")
+    assert bad != src
+    s, co = str(tmp_path / "k.hip"), str(tmp_path / "k.co")
+    open(s, "w").write(bad)
+    subprocess.run([jit.HIPCC, *jit.FLAGS, "-O1", s, "-o", co], check=True, capture_output=True)
+    data = open(co, "rb").read()
+    sig, exp = ctypes.c_uint32(), ctypes.c_uint32()
+    assert _lib.lib().nldpc_code_object_sig(data, len(data), 0, ctypes.byref(sig), ctypes.byref(exp)) == _lib.NLDPC_OK
+    assert sig.value == 0x12345678 and exp.value != sig.value
 
 
 def test_missing_hipcc_falls_back_to_streaming(monkeypatch):
