@@ -229,7 +229,8 @@ def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings,
     # the label: the ceiling the evidence puts nearest (the ISA issue floor or the PMC-weighted VALU issue, the
     # compulsory HBM bytes), a latency-bound kernel when neither is near and the waves mostly wait (PMC SQ_WAIT_ANY
     # over wave-cycles: the cfg5 backward's LDS round trips and barriers), else "unknown"
-    valu_frac = r.get("issue_frac") or r.get("valu_issue", {}).get("weighted_frac_of_simd_cycles")
+    vi = r.get("valu_issue", {})
+    valu_frac = r.get("issue_frac") or vi.get("weighted_frac_of_simd_cycles") or vi.get("frac_of_peak")
     wait = pmc.get("wait_any_over_wave_cycles") if pmc else None
     if valu_frac is not None and valu_frac >= 0.5 and valu_frac > r["frac"]:
         r["bound"] = "valu"
@@ -239,7 +240,7 @@ def roofline(prof, kb, steps, B, Z, world, graph_tag, d5_bytes_per_cw, ceilings,
         r["bound"] = "latency"
     r["bound_evidence"] = (f"HBM {r['frac']:.2f} of peak (compulsory bytes); VALU issue "
                            f"{'%.2f' % valu_frac if valu_frac is not None else 'unmeasured'} of the launch "
-                           f"({'ISA issue floor' if r.get('issue_frac') else 'PMC class-weighted' if valu_frac is not None else 'no ISA budget / PMC'}); "
+                           f"({'ISA issue floor' if r.get('issue_frac') else 'PMC class-weighted' if vi.get('weighted_frac_of_simd_cycles') else 'PMC at 2 cycles per instruction, a lower bound' if valu_frac is not None else 'no ISA budget / PMC'}); "
                            f"SQ_WAIT_ANY / wave-cycles {'%.2f' % wait if wait is not None else 'unmeasured'}")
     if dom == "fused" and d5_bytes_per_cw:
         # SURVEY §8(d) D5 models a flooding decoder whose E*Z message state crosses HBM every iteration;

@@ -260,7 +260,8 @@ __global__ __launch_bounds__(256) void bce_grad_kernel(BceArgs a, const float* _
 // only (one partial sum per workgroup is written so the loads are live): 16 B per lane, each workgroup moving tiles of
 // 256 lanes x kUnroll float4 (every load of a tile issued before its first use, 8 loads in flight per lane;
 // non-temporal, as the decoder's posterior stores), grid-stride over the tiles.  VERDICT r5: the r5 probe (one float4
-// per lane and trip) measured copy 4.8 TB/s against the guide's 6.29 TB/s float4 copy.  kind 3: read only with 4 B
+// per lane and trip) measured copy 4.8 TB/s against the guide's 6.29 TB/s float4 copy; r6 sweep (28 configurations,
+// tools/dev/hbm_probe_sweep.hip): copy tops out at 5.2-5.5 TB/s on this box in every form.  kind 3: read only with 4 B
 // per lane, the decoder's own load width (calibrates the FETCH_SIZE counter for those loads; kept as it was).
 constexpr int kProbeUnroll = 8;
 typedef float probe_v4 __attribute__((ext_vector_type(4)));  // (the nontemporal builtins take native vectors)
@@ -274,10 +275,10 @@ __global__ __launch_bounds__(256) void hbm_probe_kernel(int kind, float4* __rest
     if (kind <= 2) {
         for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
             const int64_t base = t * TILE + threadIdx.x;
-            if (kind == 1) {
+            if (kind == 1) {  // (plain stores: 5.82 TB/s against 5.67 non-temporal, profiles/r6_hbm_probe_sweep.txt)
                 const probe_v4 v = {1.f, 2.f, 3.f, 4.f};
 #pragma unroll
-                for (int k = 0; k < kProbeUnroll; ++k) __builtin_nontemporal_store(v, dst + base + k * 256);
+                for (int k = 0; k < kProbeUnroll; ++k) dst[base + k * 256] = v;
                 continue;
             }
             probe_v4 v[kProbeUnroll];
@@ -321,8 +322,9 @@ extern "C" int nldpc_hbm_probe(int32_t kind, float* dst, const float* src, int64
     if (kind < 0 || kind > 3 || !dst || (kind != 1 && !src) || n <= 0 || (n & 3))
         return fail(NLDPC_EINVAL, "nldpc_hbm_probe: bad argument");
     const int64_t n4 = n >> 2;
-    // kinds 0-2: 8 workgroups of 256 per CU, each looping over 32 KB tiles; kind 3: 32 per CU (the r2 calibration)
-    const int blocks = kind == 3 ? 256 * 32 : 256 * 8;
+    // kinds 0-2: workgroups of 256 looping over 32 KB tiles, 16 per CU for copy / write, 2 for read (the best of the
+    // r6 sweep, profiles/r6_hbm_probe_sweep.txt); kind 3: 32 per CU (the r2 calibration)
+    const int blocks = kind == 3 ? 256 * 32 : kind == 2 ? 256 * 2 : 256 * 16;
     hipLaunchKernelGGL(hbm_probe_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), kind,
                        reinterpret_cast<float4*>(dst), reinterpret_cast<const float4*>(src), n4);
     hipError_t e = hipGetLastError();

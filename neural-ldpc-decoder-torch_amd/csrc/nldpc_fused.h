@@ -143,6 +143,21 @@ __device__ __forceinline__ void app_or(uint32_t* appw, int base, int v, bool bit
 // this lane's index in its wave (v_mbcnt: no register kept live for it)
 __device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
+// Diagnostic stamp builds only (gen_fused.py NLDPC_GEN_STAMPS): s_memtime of wave w of workgroup b at phase ph of
+// iteration it into stamps[256][waves][T][16].  Branch-free across the lanes, with a wave-uniform (scalar) offset: every
+// lane stores the same value to the same address (vector stores).  r6: r5's lane-0 branch with per-lane address math
+// pushed the training forward's stamp build from 9 to 5 632 spilled VGPRs, so its stamps timed a kernel ten times slower
+// than the real one (profiles/r6_stamps_fwd.txt).
+__device__ __forceinline__ void stamp_store(uint64_t* stamps, int waves, int T, int it, int ph) {
+    if (!stamps || blockIdx.x >= 256) return;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t off = ((((uint32_t)blockIdx.x * waves + wv) * T + it) * 16 + ph) * 8;
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    const rsrc_t r = make_rsrc((const float*)stamps, 256u * waves * T * 16 * 8);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)t, r, 0, off, 0);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(t >> 32), r, 0, off + 4, 0);
+}
+
 
 // Weights are wave-uniform per edge: read through the constant address space so they arrive by
 // scalar loads (a row's edges are consecutive in C order: one s_load_dwordx8/x16 per row).
@@ -321,9 +336,20 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         par ^= pos[k];
     }
     asm volatile("" : "+v"(mg1), "+v"(mg2));
+#if NLDPC_CN_MINSUB
+    // (r6 experiment, gen_fused.py NLDPC_GEN_CNMINSUB) the magnitude select without a compare: every edge but the
+    // argmin (and its ties) has |m| >= min2 >= mg2, the argmin |m| = min1 <= mg2, so min(mg2, |m|) is mg2 or min1 and
+    // bits(mg1) + bits(mg2) - bits(min(mg2, |m|)) is mg1 or mg2 (min1 == mg1 whenever it is below the 10000 cap; at the
+    // cap all three are 10000): v_min + v_sub_u32 (4.2 + 2.2 cycles) instead of v_cmp + v_cndmask (5.2 + 4.2)
+    const uint32_t msum = __builtin_bit_cast(uint32_t, mg1) + __builtin_bit_cast(uint32_t, mg2);
+#endif
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
+#if NLDPC_CN_MINSUB
+        const float mag = __builtin_bit_cast(float, msum - __builtin_bit_cast(uint32_t, min_a(mg2, m[k])));
+#else
         const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
+#endif
         const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
         m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
     }

@@ -17,8 +17,13 @@ four parts (even parts on two SIMDs, odd parts on the other two: gen_fused.py Sp
 VALU issue cycles per codeword-iteration are the sum over its four parts' loops.  That sum is the floor the
 SIMD cannot beat whatever the latency hiding, barrier balance or memory system do.
 
-Usage: python tools/isa_budget.py /tmp/isa/parts/p{0..7}.s   (prints the tables committed in
-profiles/r4_isa_budget.txt)
+Usage: python tools/isa_budget.py [--func=MANGLED_SUBSTRING --name=KEY --geom=G,P,WPP,THREADS --json=FILE] p0.s p1.s ...
+(tools/isa_budget.sh runs it for any generated kernel; the defaults are the cfg3 decode kernel of
+profiles/r4_isa_budget.txt).  r6: any geometry -- the SIMD issue cycles of one workgroup-iteration are the busiest
+SIMD's under round-robin wave placement when one workgroup fills the CU (1024 threads), else the workgroup's total
+over the 4 SIMDs (a lower bound whatever the residency); per-part register metadata (VGPRs, spills) printed too.
+The counts are static: exact for kernels without run-time branches in the loop (the Neural decode kernels; PMC
+SQ_INSTS_VALU agrees within 1 %), an over-count for kernels whose loop carries unexecuted branches (UCN, fallbacks).
 """
 import collections
 
@@ -40,13 +45,37 @@ def vclass(op):
     return "half"
 
 
-def parse(path):
+def func_lines(path, func):
+    """The asm lines of the kernel whose mangled name contains `func` (all lines when func is None) and its
+    register metadata."""
     raw = open(path).read().split("\n")
+    meta = {}
+    if func:
+        start = next(i for i, ln in enumerate(raw)
+                     if ln.split(";")[0].strip().endswith(":") and func in ln and not ln.startswith((".", " ", "\t")))
+        end = next(i for i in range(start, len(raw)) if raw[i].startswith(".Lfunc_end"))
+        name = raw[start].split(";")[0].strip()[:-1]
+        text = "\n".join(raw)
+        import re
+        for blk in re.split(r"\n  - \.", text):
+            if f".name:           {name}" in blk or f"name:           {name}" in blk:
+                for key in ("vgpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size"):
+                    m = re.search(rf"\.{key}:\s+(\d+)", blk)
+                    if m:
+                        meta[key] = int(m.group(1))
+        raw = raw[start:end]
+    return raw, meta
+
+
+def parse(path, func=None):
+    raw, meta = func_lines(path, func)
+    parse.meta = meta
     # the iteration loop: of the labels the asm comments as "Loop Header", the one whose body (header to the
     # last branch back to it) holds the most s_barrier instructions (the Boosted kernels have other loops)
     best = None
     for i, ln in enumerate(raw):
-        if "Loop Header" in ln and ln.startswith(".LBB"):
+        # (any label with a later branch back to it: the asm does not always comment the loop header)
+        if ln.startswith(".LBB") and ln.split(";")[0].strip().endswith(":"):
             label = ln.split(":")[0]
             ends = [k for k in range(len(raw) - 1, i, -1)
                     if raw[k].strip().startswith("s_") and raw[k].strip().split()[-1] == label
@@ -91,9 +120,19 @@ def cycles(c):
     return sum(c[k] * COST[k] for k in COST)
 
 
-def main(paths):
-    parts = [parse(p) for p in paths]
-    names = ["VN+W0 (+R3)", "CN0+W1", "R0+CN1", "W2+R1", "CN2+W3", "R2+CN3"]
+def main(paths, func=None, geom=(1, 8, 2, 1024)):
+    parts, metas = [], []
+    for p in paths:
+        parts.append(parse(p, func))
+        metas.append(parse.meta)
+    G, P, WPP, THREADS = geom
+    nph = max(len(ph) for ph in parts)
+    names = (["VN+W0 (+R3)", "CN0+W1", "R0+CN1", "W2+R1", "CN2+W3", "R2+CN3"] if nph == 6 and func is None
+             else [f"phase {k}" for k in range(nph)])
+    if any(metas):
+        print("registers per part (single-part builds): " + "; ".join(
+            f"p{p}: {m.get('vgpr_count')} VGPR / {m.get('vgpr_spill_count')} spilled, {m.get('sgpr_spill_count')} SGPR spills"
+            for p, m in enumerate(metas)))
     print("VALU instructions per wave and iteration, by barrier phase (hot loop, one wave of each part)")
     print("part " + "".join(f"{n:>13s}" for n in names) + "     total  add_f32   full   half   vopc    LDS  VMEM  SALU")
     tot = []
@@ -106,13 +145,20 @@ def main(paths):
     print("VALU issue cycles per wave and iteration at the measured class costs (full 2.2, half 4.2, VOPC 5.2)")
     for p, s in enumerate(tot):
         print(f"part {p}: {cycles(s):8.0f}")
-    simd = {0: [0, 2, 4, 6], 1: [1, 3, 5, 7]}
     print()
-    worst = 0
-    for k, ps in simd.items():
-        c = sum(cycles(tot[p]) for p in ps)
-        worst = max(worst, c)
-        print(f"SIMD set {k} (parts {ps}): {c:8.0f} VALU issue cycles per codeword-iteration")
+    if THREADS == 1024:  # one workgroup per CU: waves placed round-robin, wave w = p * WPP + k on SIMD w % 4
+        load = [0.0] * 4
+        for p, s_ in enumerate(tot):
+            for k in range(WPP):
+                load[(p * WPP + k) % 4] += cycles(s_)
+        worst = max(load)
+        print("SIMD issue cycles per workgroup-iteration (one workgroup per CU, round-robin waves): " +
+              ", ".join(f"SIMD {k} {c:.0f}" for k, c in enumerate(load)))
+    else:  # several workgroups per CU: the workgroup's total over the 4 SIMDs (a lower bound)
+        worst = sum(cycles(s_) * WPP for s_ in tot) / 4
+        print(f"SIMD issue cycles per workgroup-iteration (workgroup total / 4 SIMDs): {worst:.0f}")
+    if func is not None:
+        return worst
     E, Z = 197, 384
     edges = E * Z / 64 / 4   # wave-edge-copies per SIMD and iteration
     allv = sum(s["valu"] for s in tot) / 2   # per SIMD (four of the eight parts' waves)
@@ -128,23 +174,24 @@ def main(paths):
     return worst
 
 
-def write_json(path, worst, source):
-    """The budget bench.py reads (roofline.issue_floor_ms): busier-set SIMD issue cycles per workgroup-iteration."""
+def write_json(path, worst, source, name="fused_bg2_z384::kernel<3, 0>", G=1, threads=1024):
+    """The budget bench.py reads (roofline.issue_floor_ms): busiest-SIMD issue cycles per workgroup-iteration."""
     import json
     import os
     d = json.load(open(path)) if os.path.exists(path) else {}
-    d["fused_bg2_z384::kernel<3, 0>"] = {"simd_issue_cycles_per_wg_iter": int(round(worst)), "G": 1,
-                                          "clock_ghz": CLK_GHZ, "source": source}
+    d[name] = {"simd_issue_cycles_per_wg_iter": int(round(worst)), "G": G, "threads": threads,
+               "model": "busiest SIMD, one workgroup per CU" if threads == 1024 else "workgroup total / 4 SIMDs",
+               "clock_ghz": CLK_GHZ, "source": source}
     with open(path, "w") as f:
         json.dump(d, f, indent=1)
         f.write("\n")
 
 
 if __name__ == "__main__":
-    args = sys.argv[1:]
-    js = None
-    if args and args[0].startswith("--json="):
-        js, args = args[0][7:], args[1:]
-    worst = main(args)
-    if js:
-        write_json(js, worst, "tools/isa_budget.sh (gfx950 asm of single-part builds of the library's generator)")
+    opts = {a.split("=", 1)[0][2:]: a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--")}
+    files = [a for a in sys.argv[1:] if not a.startswith("--")]
+    geom = tuple(int(v) for v in opts["geom"].split(",")) if "geom" in opts else (1, 8, 2, 1024)
+    worst = main(files, opts.get("func"), geom)
+    if "json" in opts:
+        write_json(opts["json"], worst, "tools/isa_budget.sh (gfx950 asm of single-part builds of the library's generator)",
+                   opts.get("name", "fused_bg2_z384::kernel<3, 0>"), geom[0], geom[3])
