@@ -74,17 +74,13 @@ NOBWD = os.environ.get("NLDPC_GEN_NOBWD") == "1"  # experiment builds without ba
 # SAVE kernels of one-codeword geometries: lane offsets re-derived per phase, buffer-descriptor saves (r5: the
 # cfg5 training forward 11.57 -> 11.38 ms, profiles/r5i_ab_uremat.txt); NLDPC_GEN_UREMAT=0 turns it off
 UREMAT = os.environ.get("NLDPC_GEN_UREMAT", "1") == "1"
-# backward VN-weight chains software-pipelined one deep (r6, see emit_bwd): NLDPC_GEN_BWDPIPE=1
-# 1: the degree-1 chains of the read-backs, 2: + the VN phase (loads of the next column copy before this one's carry
-# store), 3: + the VN suffix sums in LDS
-BWDPIPE = int(os.environ.get("NLDPC_GEN_BWDPIPE", "0"))
-# cfg3 check-node experiments (r6): NLDPC_GEN_CNMINSUB=1 the Neural magnitude select as v_min + v_sub_u32
-# (nldpc_fused.h NLDPC_CN_MINSUB); NLDPC_GEN_CNSCHED=V pins each row copy's interleave with sched_group_barrier: one LDS
-# read of the next row copy per V VALU of this one, then the rest of the VALU, then this row copy's LDS writes
-CNMINSUB = os.environ.get("NLDPC_GEN_CNMINSUB", "0") == "1"
-CNSCHED = int(os.environ.get("NLDPC_GEN_CNSCHED", "0"))
-# backward staging DMA of chunk c+1 issued at the start of chunk c's read-back (r6): NLDPC_GEN_BWDSTAGE=1
-BWDSTAGE = os.environ.get("NLDPC_GEN_BWDSTAGE", "0") == "1"
+# r6 backward (cfg5, profiles/r6_ab_cfg5_bwd.txt; every variant's gradients bit-identical, tools/grad_digest.py):
+#   NLDPC_GEN_BWDPIPE (default 1): the read-backs' degree-1 VN-weight chains software-pipelined one deep (25.0 -> 24.0 ms)
+#   NLDPC_GEN_CNBSPARSE (default 1): the tied kernel's check node with a third fewer VALU (nldpc_node.h NLDPC_CNB_SPARSE:
+#   QMS ordering keys, branch-free minima, sparse pass 3) and its wave sum in a register (24.0 -> 20.7 ms)
+BWDPIPE = os.environ.get("NLDPC_GEN_BWDPIPE", "1") == "1"
+CNBSPARSE = os.environ.get("NLDPC_GEN_CNBSPARSE", "1") == "1"
+TACC = CNBSPARSE
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
 # chosen by auto_geometry
@@ -689,21 +685,8 @@ def emit(S: Spec) -> str:
             for n in range(len(rcs)):
                 if n + 1 < len(rcs):
                     rc_load(n + 1)
-                if not CNSCHED:
-                    w("    __builtin_amdgcn_sched_barrier(0);")
+                w("    __builtin_amdgcn_sched_barrier(0);")
                 rc_compute(n)
-                if CNSCHED:
-                    # masks: 0x2 VALU, 0x100 DS read, 0x200 DS write (the LDS reads of row copy n+1 spread over this
-                    # row copy's arithmetic instead of issued as one burst before it)
-                    nxt = [e for e in S.row_edges[rcs[n + 1][0]] if e not in d1set] if n + 1 < len(rcs) else []
-                    cur = [e for e in S.row_edges[rcs[n][0]] if e not in d1set]
-                    w("    if constexpr (KIND == NLDPC_NEURAL) {")
-                    for _ in nxt:
-                        w(f"        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); __builtin_amdgcn_sched_group_barrier(0x2, {CNSCHED}, 0);")
-                    w("        __builtin_amdgcn_sched_group_barrier(0x2, 1000, 0);")
-                    w(f"        __builtin_amdgcn_sched_group_barrier(0x200, {max(len(cur), 1)}, 0);")
-                    w("    }")
-                    w("    __builtin_amdgcn_sched_barrier(0);")
             w("}")
 
     # ---------------------------------------------------------------- the kernel
@@ -1044,15 +1027,12 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w(f"{indent}  ctb_ += du_ * xp_;")
         w(f"{indent}  bstore(cyr, vo, {X(j, q)}, du_ * wvn[{j}]); }}")
 
-    # r6 (BWDPIPE): the chains of a phase software-pipelined one deep -- the next chain's loads are issued before
+    # r6 (BWDPIPE): the degree-1 chains of a read-back software-pipelined one deep -- the next chain's loads are issued before
     # this chain computes and stores its carry, so no load waits behind a carry store (vmcnt counts loads and stores
     # in issue order: each chain used to wait a full memory round trip behind the previous chain's store)
-    def chain_load(n, j, q, indent, gy=None, cond=None):
-        on = f"!({cond}) ? 0.f : " if cond else ""
-        w(f"{indent}const float xp{n}_ = {on}it >= 1 ? bload(sxp, vo, {X(j, q)}) : bload(xr, vo, {X(j, q)});")
-        w(f"{indent}const float cy{n}_ = {on}it == a.T - 1 ? 0.f : bload(cyr, vo, {X(j, q)});")
-        if gy:
-            w(f"{indent}const float gy{n}_ = it >= 1 ? gy_masked<KIND>({gy}, vo, vm, {X(j, q)}) : 0.f;")
+    def chain_load(n, j, q, indent):
+        w(f"{indent}const float xp{n}_ = it >= 1 ? bload(sxp, vo, {X(j, q)}) : bload(xr, vo, {X(j, q)});")
+        w(f"{indent}const float cy{n}_ = it == a.T - 1 ? 0.f : bload(cyr, vo, {X(j, q)});")
 
     def chain_pre(n, j, q, gsum, indent):
         w(f"{indent}{{ const float xp_ = xp{n}_;")
@@ -1126,79 +1106,15 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
             w("}")
 
     # ---------------------------------------------------------------- variable-node backward
-    # BWDPIPE >= 2: the suffix sums of a column copy go through a per-thread LDS column (k * threads + t) in the chunk
-    # images, free during the VN phase (a barrier before the next iteration's first owner write), instead of d
-    # registers on top of the state (the degree-23 column of part 0 peaked there)
-    maxd = max([len(S.col_edges[j]) for c_ in S.reg_cols for j in c_] or [1])
-    suf_lds = BWDPIPE >= 3 and maxd * S.threads <= S.chunk_floats * S.G_lds
     for p in range(S.P):
         w("template <int KIND, int TIED>")
         w(f"__device__ __forceinline__ void vnb_p{p}({state_params(p)}, const FusedBwdArgs& a, "
           f"int it, uint32_t vo, uint32_t vm, rsrc_t gr, rsrc_t mr, rsrc_t xr, rsrc_t sxp, rsrc_t cyr, cfloat_p wvn, "
-          f"int64_t pv, bool lane0, bool dup_, float* sfl) {{")
+          f"int64_t pv, bool lane0, bool dup_) {{")
         w("    const bool chain_on = KIND != NLDPC_NEURAL && a.w_vn;")
         w("    const QRange qr = q_range(a.qbit);")
         s0 = 0
-        if BWDPIPE >= 2 and S.reg_cols[p]:
-            # (r6: per column copy n: compute, then the loads of copy n+1, then copy n's carry store -- no load waits
-            # behind a carry store, and the next copy's loaded values are not live across this copy's suffix sums,
-            # the phase's register peak.  Issuing them before the compute instead spilled 109 VGPRs.)
-            items, s_ = [], 0
-            for j in S.reg_cols[p]:
-                d = len(S.col_edges[j])
-                items += [(j, q, s_, d) for q in range(Q)]
-                s_ += d
-            # (one code path: a run-time branch around the whole phase made two copies of it and the allocator spilled
-            # 1 500 VGPRs at their join)
-            chain_load(0, items[0][0], items[0][1], "        ", gy="gr, mr", cond="chain_on")
-            w("        float ctb_;")
-            for n, (j, q, s0, d) in enumerate(items):
-                c = lambda k: sref(q, s0 + k)  # noqa: E731
-                if q == 0:
-                    w(f"        ctb_ = 0.f;  // column {j}, degree {d}")
-                w(f"        float cyo{n}_ = 0.f;")
-                w("        {")
-                w("            float gs_ = 0.f;")
-                for k in range(d):
-                    w(f"            gs_ = gs_ + {c(k)};")
-                w("            if (it >= 1) {")
-                w(f"                const float gyv_ = gy{n}_;")
-                if suf_lds:  # suf_[k] for k = 1 .. d-1 in LDS (suf_[d] = 0; suf_[0] is not used)
-                    w("                float sf_ = 0.f;")
-                    for k in range(d - 1, 0, -1):
-                        w(f"                sf_ = sf_ + {c(k)}; sfl[{k * S.threads}] = sf_;")
-                    w("                float pre_ = 0.f;")
-                    for k in range(d):
-                        sk = "0.f" if k + 1 == d else f"sfl[{(k + 1) * S.threads}]"
-                        w(f"                {{ const float o_ = {c(k)}; {c(k)} = gyv_ + (pre_ + {sk}); pre_ += o_; }}")
-                else:
-                    w(f"                float suf_[{d + 1}];")
-                    w(f"                suf_[{d}] = 0.f;")
-                    for k in range(d - 1, -1, -1):
-                        w(f"                suf_[{k}] = suf_[{k + 1}] + {c(k)};")
-                    w("                float pre_ = 0.f;")
-                    for k in range(d):
-                        w(f"                {{ const float o_ = {c(k)}; {c(k)} = gyv_ + (pre_ + suf_[{k + 1}]); pre_ += o_; }}")
-                w("            }")
-                w("            if (chain_on) {")
-                w(f"                const float xp_ = xp{n}_;")
-                w(f"                const float u_ = fmul(xp_, wvn[{j}]);")
-                w("                const float mk_ = (KIND == NLDPC_QMS && qr.active) ? in_range(u_, qr.lo, qr.hi) : 1.f;")
-                w(f"                const float du_ = (gs_ + cy{n}_) * mk_;")
-                w("                ctb_ += du_ * xp_;")
-                w(f"                cyo{n}_ = du_ * wvn[{j}];")
-                w("            }")
-                w("        }")
-                w("        __builtin_amdgcn_sched_barrier(0);")
-                if n + 1 < len(items):
-                    chain_load(n + 1, items[n + 1][0], items[n + 1][1], "        ", gy="gr, mr", cond="chain_on")
-                w(f"        if (chain_on) bstore(cyr, vo, {X(j, q)}, cyo{n}_);")
-                w("        __builtin_amdgcn_sched_barrier(0);  // one column copy at a time (register pressure)")
-                if q == Q - 1:
-                    w("        if (chain_on) {")
-                    col_partial(j, "            ")
-                    w("        }")
-        for j in S.reg_cols[p] if not (BWDPIPE >= 2 and S.reg_cols[p]) else []:
+        for j in S.reg_cols[p]:
             d = len(S.col_edges[j])
             w(f"    {{  // column {j}, degree {d}")
             w("        float ctb_ = 0.f;")
@@ -1239,7 +1155,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     SBY = S.stage
     w("template <int KIND, int DC, int TIED, int Q0, int Q1>  // the row's copies Q0 .. Q1-1")
     w("__device__ __forceinline__ void cnb_row(float* rp, const char* sq, int u, const FusedBwdArgs& a, int it, "
-      "int e0, int row, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
+      "int e0, int row, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc, float& tacc) {")
     # a scheduling fence after each lane copy, none per row: the row fence pushed the tied QMS kernel to 123
     # VGPR spills (21 without) and cfg5's backward measured 27.97 -> 27.32 ms without it (no fence at all:
     # 27.49; profiles/r4_ab.txt)
@@ -1320,10 +1236,16 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         # no reduction inside the row loop, made the register allocator spill 5 520 VGPRs)
         w(f"{indent}if constexpr (TIED) {{")
         w(f"{indent}    float t_ = 0.f;")
+        if CNBSPARSE:  # (the tied MS / QMS check node keeps its sum in gwa[0], started from +0: 0 + gwa[0] + 0 ... is gwa[0])
+            w(f"{indent}    if constexpr (KIND == NLDPC_MS || KIND == NLDPC_QMS) t_ = gwa[0];")
+            w(f"{indent}    else")
         w("#pragma unroll")
         w(f"{indent}    for (int k = 0; k < DC; ++k) t_ += gwa[k];")
         w(f"{indent}    const float s_ = wave_sum(dup_ ? 0.f : t_);")
-        w(f"{indent}    if (lane0) gacc[0] += s_;")
+        if TACC:  # (r6: the wave's running sum in a register -- no LDS read-add-write by lane 0 per row copy)
+            w(f"{indent}    tacc += s_;")
+        else:
+            w(f"{indent}    if (lane0) gacc[0] += s_;")
         w(f"{indent}}} else {{")
     tied("        ")
     flush_q("            ")
@@ -1335,7 +1257,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         for ci, (r0, r1, e0c, e1c) in enumerate(S.chunks):
             w("template <int KIND, int TIED>")
             w(f"__device__ __forceinline__ void cnb_p{p}_c{ci}(float* lds, const char* stg, int u, const FusedBwdArgs& a, "
-              "int it, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc) {")
+              "int it, rsrc_t svr, uint32_t vcw, int64_t pc, bool lane0, bool dup_, float* gacc, float& tacc) {")
             w("    asm volatile(\"\" : \"+v\"(u));")
             w("    constexpr int SB = saved_msg_bytes<KIND>();")
             # whole rows per part (untied: a row's per-edge sums add up over its copies in the wave's LDS
@@ -1347,13 +1269,13 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 es = S.row_edges[i]
                 off = (es[0] - e0c) * Z
                 w(f"        cnb_row<KIND, {len(es)}, 0, 0, {Q}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, svr, "
-                  "vcw, pc, lane0, dup_, gacc);")
+                  "vcw, pc, lane0, dup_, gacc, tacc);")
             w("    } else {")
             for i in rows:
                 es = S.row_edges[i]
                 off = (es[0] - e0c) * Z
                 w(f"        cnb_row<KIND, {len(es)}, 1, 0, {Q}>(lds + {off} + u, stg + ({off} + u) * SB, u, a, it, {es[0]}, {i}, "
-                  "svr, vcw, pc, lane0, dup_, gacc);")
+                  "svr, vcw, pc, lane0, dup_, gacc, tacc);")
             w("    }")
             w("}")
             # the chunk's saved block -> this codeword's staging region (all threads of the workgroup)
@@ -1388,7 +1310,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w("template <int KIND, int TIED>")
         w(f"__device__ __forceinline__ void bwd_p{p}(const FusedBwdArgs& a, float* lds, int u, int64_t blk, int nlive, "
           f"uint32_t vo, uint32_t vm, uint32_t vcw, int slot, bool lane0, bool dup_, const char* stg, char* stg_all, "
-          f"float* gacc, int wb, float* lds_all_) {{")
+          f"float* gacc, int wb) {{")
         for q in range(Q):
             w(f"    float g{q}[{sp}];")
         w(f"    const rsrc_t cyr = make_rsrc(a.carry ? a.carry + blk * {NZ} : nullptr, a.carry ? nlive * {4 * NZ} : 0);")
@@ -1430,29 +1352,19 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 assert ph < 16
                 w(f"        stamp_store(a.stamps, {S.threads // 64}, a.T, it, {ph});")
         w("        if (TIED && lane0) gacc[0] = 0.f;  // (tied CN: the wave's sum lives in its LDS slot)")
+        w("        float tacc = 0.f;  // (TACC: the tied CN's wave sum in a register instead)")
         bstamp(0)
         for ci in range(len(S.chunks)):
-            if SBY and not (BWDSTAGE and ci > 0):  # the chunk's saved messages start moving into LDS now and land by the barrier
-                if BWDSTAGE:  # (chunk 0: issued in the previous iteration's last read-back, but for the first one)
-                    w(f"        if (it == a.T - 1) stage_c{ci}<KIND>(a, it, blk, nlive, stg_all, wb);")
-                else:
-                    w(f"        stage_c{ci}<KIND>(a, it, blk, nlive, stg_all, wb);")
+            if SBY:  # the chunk's saved messages start moving into LDS now and land by the barrier
+                w(f"        stage_c{ci}<KIND>(a, it, blk, nlive, stg_all, wb);")
             w(f"        wrb_p{p}_c{ci}<KIND>({state_args()}, lds, u, gr, mr, vo, vm);")
             bstamp(1 + 3 * ci)
             if SBY:
                 w("        asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // (LDS-DMA: not in hipcc's count)")
             w("        __syncthreads();")
-            w(f"        cnb_p{p}_c{ci}<KIND, TIED>(lds, stg, u, a, it, svr, vcw, pc, lane0, dup_, gacc);")
+            w(f"        cnb_p{p}_c{ci}<KIND, TIED>(lds, stg, u, a, it, svr, vcw, pc, lane0, dup_, gacc, tacc);")
             bstamp(2 + 3 * ci)
             w("        __syncthreads();")
-            if SBY and BWDSTAGE:
-                # r6 (BWDSTAGE): the next chunk's saved messages go out at the start of this read-back -- every check
-                # node of this chunk has read the staging region (barrier above), and the DMA then no longer queues
-                # behind the read-back's carry stores (vmcnt counts in issue order)
-                if ci + 1 < len(S.chunks):
-                    w(f"        stage_c{ci + 1}<KIND>(a, it, blk, nlive, stg_all, wb);")
-                else:
-                    w(f"        if (it >= 1) stage_c0<KIND>(a, it - 1, blk, nlive, stg_all, wb);")
             w(f"        rdb_p{p}_c{ci}<KIND, TIED>({state_args()}, lds, u, a, it, vo, xr, sxp, cyr, wvn, pv, lane0, dup_);")
             bstamp(3 + 3 * ci)
             w("        __syncthreads();")
@@ -1460,15 +1372,12 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w("        const uint8_t* mq_ = (a.symask && it >= 1) ? a.symask + (it - 1) * a.symask_stride : nullptr;")
         w(f"        const rsrc_t gr1 = {rs('gq_', 4, NZ)};")
         w(f"        const rsrc_t mr1 = {rs('mq_', 1, NZ)};")
-        w(f"        vnb_p{p}<KIND, TIED>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0, dup_, "
-          f"lds_all_ + threadIdx.x);")
+        w(f"        vnb_p{p}<KIND, TIED>({state_args()}, a, it, vo, vm, gr1, mr1, xr, sxp, cyr, wvn, pv, lane0, dup_);")
         # tied weights: the wave's sums into the part's designated entries (written 0 earlier this iteration,
         # by this wave's lane 0: program order makes these the final values)
         # (the launcher zeroed the tied kernel's partials: each part's wave total goes to the part's own entry
         # p of the row -- distinct per part, and the two waves of a part have slots of their own)
-        w(f"        if (TIED && a.p_cn && lane0) a.p_cn[pc + {p}] = gacc[0];")
-        if suf_lds:  # (the suffix columns live in the chunk images: every wave's VN phase is done before they are reused)
-            w("        __syncthreads();")
+        w(f"        if (TIED && a.p_cn && lane0) a.p_cn[pc + {p}] = {'tacc' if TACC else 'gacc[0]'};")
 
         bstamp(1 + 3 * len(S.chunks))
         w("    }")
@@ -1515,7 +1424,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w(f"    for (int i = t; i < {STF}; i += {S.threads}) ((float*)(stg_all + {G * 4 * STF}))[i] = 0.f;")
     for n_, p in enumerate(PARTS or range(S.P)):  # (NLDPC_GEN_PARTS: single-part builds for the ISA budget)
         w(f"    {'if' if n_ == 0 else 'else if'} (p == {p}) bwd_p{p}<KIND, TIED>(a, lds, u, blk, nlive, vo, vm, vcw, slot, lane0, dup_, "
-          "stg, stg_all, gacc, wb, lds_all);")
+          "stg, stg_all, gacc, wb);")
     w("}")
     # a tied CN weight (cfg5's NW(3,0,3): one CN weight per iteration): a separate kernel (TIED = 1) reduces
     # each row copy's contributions once (one wave reduction per row copy into the wave's LDS sum) instead of
@@ -1552,8 +1461,8 @@ def jit_source(hb, Z, kind, mode):
     G, P, Q = auto_geometry(hb, Z)
     S = Spec("jit", hb, Z, G, P, Q, sched="pipe2" if mode in (0, 2, 3) else "one",  # the SAVE kernels keep one buffer
              stage=BWD_STAGE[kind] if mode == 4 else 0)  # (backward: staged saved messages)
-    L = ["// GENERATED by gen_fused.py jit_source -- do not edit.", "#include <hip/hip_runtime.h>",
-         '#include "nldpc_fused.h"', "namespace nldpc {", emit(S) if mode < 4 else emit_bwd(S, BWD_NS[kind]),
+    L = ["// GENERATED by gen_fused.py jit_source -- do not edit.", "#include <hip/hip_runtime.h>"] + \
+        (["#define NLDPC_CNB_SPARSE 1"] if CNBSPARSE else []) + ['#include "nldpc_fused.h"', "namespace nldpc {", emit(S) if mode < 4 else emit_bwd(S, BWD_NS[kind]),
          "}  // namespace nldpc"]
     lb = f"__launch_bounds__({S.threads}, {(S.threads + 255) // 256})"
     if mode < 4:
@@ -1594,8 +1503,8 @@ def main():
         specs.append((Spec(tag, hb, Z, G, P, Q, sched="pipe2"), Spec(tag, hb, Z, G, P, Q), not only or tag in only))
     head = ["// GENERATED by gen_fused.py from the base graphs in resources/ -- do not edit.",
             "#include <hip/hip_runtime.h>"]
-    if CNMINSUB:
-        head.append("#define NLDPC_CN_MINSUB 1")
+    if CNBSPARSE:
+        head.append("#define NLDPC_CNB_SPARSE 1")
     head += ['#include "nldpc_fused.h"', "namespace nldpc {"]
     kinds = os.environ.get("NLDPC_GEN_KINDS")  # debug: instantiate a subset of kinds
     kinds = [int(k) for k in kinds.split(",")] if kinds else [0, 1, 2, 3]

@@ -302,7 +302,8 @@ __device__ __forceinline__ void two_smallest_abs3(const float (&m)[DC], float& m
 // 0 to -20000 (magnitude above the 10000 clamp, not positive) and tracks the minimum again.  Bit-identical
 // to cn_core (tests compare the fused and streaming paths).  Measured r3/r4 alternatives, all bit-exact and
 // slower on the cfg3 kernel (profiles/r3b_ab.txt, r4_ab.txt): an integer key per edge (4 %), the magnitude
-// select as sat(a + b - |m|) + v_med3_u32 (48.9 -> 51.4 ms) or as min(|m|, mg2) + v_sub_u32 (51.5 ms),
+// select as sat(a + b - |m|) + v_med3_u32 (48.9 -> 51.4 ms) or as min(|m|, mg2) + v_sub_u32 (51.5 ms; r6: 49.7 ms, and
+// 48.5-48.8 ms -- a tie -- with each row copy's interleave pinned by sched_group_barrier, profiles/r6_ab_cfg3_cn.txt),
 // signs by bit arithmetic (noise), two row copies with a packed epilogue.
 template <int DC>
 __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC], const float (&b)[DC]) {
@@ -336,20 +337,9 @@ __device__ __forceinline__ void neural_row(float (&m)[DC], const float (&w)[DC],
         par ^= pos[k];
     }
     asm volatile("" : "+v"(mg1), "+v"(mg2));
-#if NLDPC_CN_MINSUB
-    // (r6 experiment, gen_fused.py NLDPC_GEN_CNMINSUB) the magnitude select without a compare: every edge but the
-    // argmin (and its ties) has |m| >= min2 >= mg2, the argmin |m| = min1 <= mg2, so min(mg2, |m|) is mg2 or min1 and
-    // bits(mg1) + bits(mg2) - bits(min(mg2, |m|)) is mg1 or mg2 (min1 == mg1 whenever it is below the 10000 cap; at the
-    // cap all three are 10000): v_min + v_sub_u32 (4.2 + 2.2 cycles) instead of v_cmp + v_cndmask (5.2 + 4.2)
-    const uint32_t msum = __builtin_bit_cast(uint32_t, mg1) + __builtin_bit_cast(uint32_t, mg2);
-#endif
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-#if NLDPC_CN_MINSUB
-        const float mag = __builtin_bit_cast(float, msum - __builtin_bit_cast(uint32_t, min_a(mg2, m[k])));
-#else
         const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
-#endif
         const float r = relu_mask(fadd(fmul(mag, w[k]), b[k]));
         m[k] = (par != pos[k]) ? r : -r;  // x * (+-1): an exact sign flip
     }

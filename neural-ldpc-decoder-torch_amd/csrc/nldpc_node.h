@@ -12,6 +12,11 @@
 #include "nldpc_math.h"
 #include "nldpc_sleef.h"
 
+// gen_fused.py defines NLDPC_CNB_SPARSE 1 in the generated backward units (the tied check node of cn_bwd_ms, r6)
+#ifndef NLDPC_CNB_SPARSE
+#define NLDPC_CNB_SPARSE 0
+#endif
+
 namespace nldpc {
 
 // ---- sum-product check node arithmetic, value for value the reference's CPU tensors
@@ -486,6 +491,45 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
     float min1 = kMaskMag, min2 = kMaskMag;
     int idx1 = -1, idx2 = -1;
     uint32_t npos = 0, posm = 0, negm = 0, mskm = 0;
+    // r6 (gen_fused.py NLDPC_GEN_CNBSPARSE): the tied kernel's check node with fewer VALU (below); the untied kernel
+    // keeps the r5 form (the same edits there spilled 204 VGPRs)
+    constexpr bool kSparse = NLDPC_CNB_SPARSE && SAMEW;
+    if constexpr (kSparse && KIND == NLDPC_QMS && DC >= 2 && DC <= 16) {
+        // (r6) QMS pass 1 on ordering keys: every conditioned input is a decoded int8 code (a multiple of 0.5 below 17,
+        // a few mantissa bits) or the zero fix 1e-4, so (bits(|x|) & ~15) | k orders the edges by |x| with the first
+        // index winning ties -- torch.min's argmin -- and the two smallest keys (v_min_u32 / v_med3_u32, two ops per
+        // edge) give both minima and both indices: no compare-and-select chain per edge.  The STE mask as one compare
+        // (clamp(x) == x), x never 0 after the zero fix so x < 0 is !(x > 0).  Bit-identical inputs to passes 2 and 3.
+        uint32_t ka = 0, kb = 0;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const float xd = load_m(k);
+            const float xc = __builtin_amdgcn_fmed3f(xd, qr.lo, qr.hi);
+            const uint32_t msk = xc == xd;
+            const float x = xc == 0.f ? kZeroFix : xc;
+            const uint32_t pos = x > 0.f;
+            npos ^= pos;
+            posm |= pos << k;
+            mskm |= msk << k;
+            const uint32_t key = (__builtin_bit_cast(uint32_t, fabsf(x)) & ~15u) | (uint32_t)k;
+            if (k == 0) {
+                ka = key;
+            } else if (k == 1) {
+                kb = max(ka, key);
+                ka = min(ka, key);
+            } else {
+                asm("v_med3_u32 %0, %1, %2, %3" : "=v"(kb) : "v"(ka), "v"(kb), "v"(key));
+                ka = min(ka, key);
+            }
+        }
+        negm = ~posm & ((1u << DC) - 1u);
+        idx1 = (int)(ka & 15u);
+        idx2 = (int)(kb & 15u);
+        constexpr uint32_t kZf = 0x38D1B717u;  // bits of kZeroFix (1e-4f): the one conditioned value with low bits set
+        static_assert(__builtin_bit_cast(uint32_t, kZeroFix) == kZf, "zero-fix constant");
+        min1 = (ka & ~15u) == (kZf & ~15u) ? kZeroFix : __builtin_bit_cast(float, ka & ~15u);
+        min2 = (kb & ~15u) == (kZf & ~15u) ? kZeroFix : __builtin_bit_cast(float, kb & ~15u);
+    } else {
 #pragma unroll
     for (int k = 0; k < DC; ++k) {  // pass 1: conditioned inputs, minima, signs, STE masks
         float x = load_m(k);
@@ -503,6 +547,19 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
         posm |= pos << k;
         negm |= (uint32_t)(x < 0.f) << k;
         mskm |= (uint32_t)msk << k;
+        if constexpr (kSparse) {
+        // (r6) branch-free: the nested ifs compiled to exec-mask branches with v_mov copies of the four trackers at
+        // every edge (60 VALU per edge copy in the tied QMS kernel).  MS / QMS inputs are never 0 after the zero fix,
+        // so only Neural needs the ax > 0 test (a NaN fails every compare either way).  lt1 implies lt2 (min1 <= min2).
+            const bool ok = KIND == NLDPC_NEURAL ? ax > 0.f : true;
+            const bool lt1 = ok && ax < min1, lt2 = ok && ax < min2;
+            const float t2 = lt2 ? ax : min2;
+            const int i2 = lt2 ? k : idx2;
+            min2 = lt1 ? min1 : t2;
+            idx2 = lt1 ? idx1 : i2;
+            min1 = lt1 ? ax : min1;
+            idx1 = lt1 ? k : idx1;
+        } else {
         if (ax > 0.f) {
             if (ax < min1) {
                 min2 = min1;
@@ -514,6 +571,8 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
                 idx2 = k;
             }
         }
+        }
+    }
     }
     float g_at1 = 0.f, g_at2 = 0.f;
     if constexpr (SAMEW && KIND != NLDPC_NEURAL) {
@@ -534,7 +593,10 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
             const float mag = sel ? magB : magA;
             const float sgn = ((npos ^ (posm >> k)) & 1u) ? 1.f : -1.f;
             const float x = fmul(mag, sgn);
-            const float s = signf_t(x), ax = fabsf(x);
+            // (r6 sparse) QMS: mag >= 0 (the minima are >= the zero fix 1e-4), so sign(x) is sgn, or 0 with mag == 0,
+            // where x1 = 0 and the relu mask makes g1 a zero either way (its sign is lost in the +0-started sums)
+            const float s = (kSparse && KIND == NLDPC_QMS) ? sgn : signf_t(x);
+            const float ax = kSparse ? fabsf(mag) : fabsf(x);  // (|mag * (+-1)| == |mag|: no multiply for it)
             const float gc = lds[k * stride];
             const float g1 = (gc * s) * (sel ? mB : mA);
             float gabs;
@@ -545,9 +607,11 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
                 // order from 0 (cnb_row), and 0 + ... + g1_k ax_k in edge order is that sum bit for bit (a
                 // partial sum from +0 is never -0, so adding +-0 terms directly or as 0 + term is the same)
                 gwa[0] += g1 * ax;
-                gabs = g1 * wc[k];
+                gabs = g1 * wc[kSparse ? 0 : k];  // (r6 sparse: the tied contract -- the row is wc[0] -- one scalar)
             }
-            const float gmag = (gabs * s) * sgn;
+            // (r6 sparse) s = sgn, or s = 0 with a zero magnitude, where g1 and gabs are +-0: (gabs * s) * sgn == gabs up
+            // to the sign of a zero, which the +0-started sums g_at1 / g_at2 never keep
+            const float gmag = kSparse ? gabs : (gabs * s) * sgn;
             if (sel) g_at2 += gmag;
             else g_at1 += gmag;
         }
@@ -587,11 +651,25 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
         else g_at1 += gmag;
     }
     }
+    if constexpr (kSparse) {
+    // (r6) pass 3 sparse: every edge gets 0, then the two argmins their value at a per-lane LDS address -- (gl * smq) *
+    // msk of the dense form for those two, +0 instead of a -0 for the others (every consumer adds them to a sum
+    // started from +0: the owners' VN backward and the degree-1 chains)
+#pragma unroll
+    for (int l = 0; l < DC; ++l) lds[l * stride] = 0.f;
+    auto put = [&](int l, float gl) {
+        const float smq = ((posm >> l) & 1u) ? 1.f : (((negm >> l) & 1u) ? -1.f : 0.f);
+        lds[l * stride] = (gl * smq) * (((mskm >> l) & 1u) ? 1.f : 0.f);
+    };
+    if (idx1 >= 0) put(idx1, g_at1);
+    if (idx2 >= 0) put(idx2, g_at2);
+    } else {
 #pragma unroll
     for (int l = 0; l < DC; ++l) {  // pass 3: the two argmins receive the gradient
         const float gl = l == idx1 ? g_at1 : (l == idx2 ? g_at2 : 0.f);
         const float smq = ((posm >> l) & 1u) ? 1.f : (((negm >> l) & 1u) ? -1.f : 0.f);
         lds[l * stride] = (gl * smq) * (((mskm >> l) & 1u) ? 1.f : 0.f);
+    }
     }
 }
 

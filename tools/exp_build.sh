@@ -17,6 +17,9 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-ma
 # reuses them, one whose headers differ gets its own)
 HW="nldpc_graph.cpp nldpc_profile.cpp nldpc_forward.hip nldpc_backward.hip nldpc_aux.hip"
 KEY=$( (cat $HW *.h $R/include/nldpc.h; echo "$FLAGS") | sha1sum | cut -c1-16)
+# HWKEY=<key>: reuse an existing hand-written build (lib_exp/.hw/<key>) -- only when the header edits since it change no
+# struct layout or code those units compile (e.g. code behind a generator macro); the layout signature still guards
+KEY=${HWKEY:-$KEY}
 HWD=$P/lib_exp/.hw/$KEY
 hpids=""
 if [ -f $HWD/done ]; then
