@@ -81,6 +81,19 @@ UREMAT = os.environ.get("NLDPC_GEN_UREMAT", "1") == "1"
 BWDPIPE = os.environ.get("NLDPC_GEN_BWDPIPE", "1") == "1"
 CNBSPARSE = os.environ.get("NLDPC_GEN_CNBSPARSE", "1") == "1"
 TACC = CNBSPARSE
+# r6 cache policies (profiles/r6_ab_cfg5_cache.txt): NLDPC_GEN_BWDCACHE (default 2) -- the backward's VN-weight carry
+# stored temporal (1) and its per-iteration streams (xin, dL/dy, masks, staged messages) loaded non-temporal (2), so the
+# carry's read-back one iteration later hits L2 (nldpc_fused.h bload_nt / gy_masked_nt / bstore_keep): backward 20.8 ->
+# 20.3 ms, fetch 36.5 -> 27.9 GB; NLDPC_GEN_FWDNT8 (default 1) -- the training forward's byte stores (clamp masks, QMS
+# saved codes) non-temporal like its fp32 stores: they were evicting the channel values its posteriors re-read (fetch
+# 9.8 -> 1.8 GB, 10.3 -> 9.7 ms)
+BWDCACHE = int(os.environ.get("NLDPC_GEN_BWDCACHE", "2"))
+_CY_ST = "bstore_keep" if BWDCACHE >= 1 else "bstore"
+_LD_NT = "bload_nt" if BWDCACHE >= 2 else "bload"
+_GY = "gy_masked_nt" if BWDCACHE >= 2 else "gy_masked"
+FWDNT8 = os.environ.get("NLDPC_GEN_FWDNT8", "1") == "1"  # (see nldpc_fused.h bstore8_nt)
+_S8 = "bstore8_nt" if FWDNT8 else "bstore8"
+_SI8 = "bstore_i8_nt" if FWDNT8 else "bstore_i8"
 
 # (tag, base graph file, Z, codewords per workgroup G, parts P, copies per thread Q); G/P/Q None =
 # chosen by auto_geometry
@@ -457,7 +470,7 @@ def emit(S: Spec) -> str:
                     w("                bool m_;")
                     w(f"                y_ = posterior_m<KIND>(xo_, P_s{q}, a, m_);")
                     w(f"                bstore(pr, vo, {X(j, q)}, y_);")
-                    w(f"                bstore8(pm, vm, {X(j, q) // 4}, m_);")
+                    w(f"                {_S8}(pm, vm, {X(j, q) // 4}, m_);")
                     w("            } else {")
                     w(f"                y_ = posterior<KIND>(xo_, P_s{q}, a);")
                     w(f"                put_post<CM>(pr, vo, {X(j, q)}, y_, ps);")
@@ -614,7 +627,7 @@ def emit(S: Spec) -> str:
                 # (one-codeword geometries: the codeword's element offset is u itself, no other value kept live)
                 eo = "(uint32_t)u" if S.uremat else "(vc >> 2)"
                 for k, e in enumerate(es):
-                    w(f"            if constexpr (KIND == NLDPC_QMS) bstore_i8(sv, {eo} + {q * ZT}u, {e * Z}, qms_code_p(m{n}[{k}], a.qp));")
+                    w(f"            if constexpr (KIND == NLDPC_QMS) {_SI8}(sv, {eo} + {q * ZT}u, {e * Z}, qms_code_p(m{n}[{k}], a.qp));")
                     w(f"            else bstore(sv, 4u * {eo} + {4 * q * ZT}u, {4 * e * Z}, m{n}[{k}]);")
                 w("        }")
                 w(f"        float wv[{DC}], bv[{DC}];")
@@ -661,7 +674,7 @@ def emit(S: Spec) -> str:
                         # the training forward: the clamp mask (byte offset = the float offset / 4) and this
                         # iteration's xin too (the owners keep no degree-1 state)
                         w("                if constexpr (SAVE) { bool m_; "
-                          f"y_ = posterior_m<KIND>(xo_, {pm}, a, m_); bstore8(nm, (vo + dv_ + {4 * (j * Z + c)}u) >> 2, 0, m_); "
+                          f"y_ = posterior_m<KIND>(xo_, {pm}, a, m_); {_S8}(nm, (vo + dv_ + {4 * (j * Z + c)}u) >> 2, 0, m_); "
                           f"bstore(sxd, vo + dv_, {4 * (j * Z + c)}, cd[{ix}]); }}")
                         w(f"                else y_ = posterior<KIND>(xo_, {pm}, a);")
                         w(f"                if (a.ucn) {bit_set('cdm', ix, 'y_ >= 0.f')};")
@@ -1019,19 +1032,19 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
     # registers are all taken by the state) and this column's weight-gradient contribution
     # (vnb_kernel's arithmetic: u = xprev * w, STE mask of Q on u, du = (gsum + carry) * mask)
     def chain(p, j, q, gsum, indent):
-        w(f"{indent}{{ const float xp_ = it >= 1 ? bload(sxp, vo, {X(j, q)}) : bload(xr, vo, {X(j, q)});")
+        w(f"{indent}{{ const float xp_ = it >= 1 ? {_LD_NT}(sxp, vo, {X(j, q)}) : {_LD_NT}(xr, vo, {X(j, q)});")
         w(f"{indent}  const float u_ = fmul(xp_, wvn[{j}]);")
         w(f"{indent}  const float mk_ = (KIND == NLDPC_QMS && qr.active) ? in_range(u_, qr.lo, qr.hi) : 1.f;")
         w(f"{indent}  const float cy_ = it == a.T - 1 ? 0.f : bload(cyr, vo, {X(j, q)});")
         w(f"{indent}  const float du_ = ({gsum} + cy_) * mk_;")
         w(f"{indent}  ctb_ += du_ * xp_;")
-        w(f"{indent}  bstore(cyr, vo, {X(j, q)}, du_ * wvn[{j}]); }}")
+        w(f"{indent}  {_CY_ST}(cyr, vo, {X(j, q)}, du_ * wvn[{j}]); }}")
 
     # r6 (BWDPIPE): the degree-1 chains of a read-back software-pipelined one deep -- the next chain's loads are issued before
     # this chain computes and stores its carry, so no load waits behind a carry store (vmcnt counts loads and stores
     # in issue order: each chain used to wait a full memory round trip behind the previous chain's store)
     def chain_load(n, j, q, indent):
-        w(f"{indent}const float xp{n}_ = it >= 1 ? bload(sxp, vo, {X(j, q)}) : bload(xr, vo, {X(j, q)});")
+        w(f"{indent}const float xp{n}_ = it >= 1 ? {_LD_NT}(sxp, vo, {X(j, q)}) : {_LD_NT}(xr, vo, {X(j, q)});")
         w(f"{indent}const float cy{n}_ = it == a.T - 1 ? 0.f : bload(cyr, vo, {X(j, q)});")
 
     def chain_pre(n, j, q, gsum, indent):
@@ -1041,7 +1054,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         w(f"{indent}  const float cy_ = cy{n}_;")
         w(f"{indent}  const float du_ = ({gsum} + cy_) * mk_;")
         w(f"{indent}  ctb_ += du_ * xp_;")
-        w(f"{indent}  bstore(cyr, vo, {X(j, q)}, du_ * wvn[{j}]); }}")
+        w(f"{indent}  {_CY_ST}(cyr, vo, {X(j, q)}, du_ * wvn[{j}]); }}")
 
     def col_partial(j, indent):  # (lanes repeating a live one add nothing: Spec.lanes_pad)
         # (a tied VN weight keeps these: one wave reduction per column either way; a per-lane running sum over
@@ -1062,7 +1075,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                     w(f"    lds[{own(e, q, e0)}] = {sref(q, k)};")
             for j, e in d1:  # dL/dc2v_{k+1} of a degree-1 edge: only its own posterior
                 for q in range(Q):
-                    w(f"    lds[{own(e, q, e0)}] = gy_masked<KIND>(gr, mr, vo, vm, {X(j, q)});")
+                    w(f"    lds[{own(e, q, e0)}] = {_GY}<KIND>(gr, mr, vo, vm, {X(j, q)});")
             w("}")
             w("template <int KIND, int TIED>")
             w(f"__device__ __forceinline__ void rdb_p{p}_c{ci}({state_params(p)}, const float* lds, "
@@ -1125,7 +1138,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 for k in range(d):
                     w(f"            gs_ = gs_ + {c(k)};")
                 w("            if (it >= 1) {")
-                w(f"                const float gyv_ = gy_masked<KIND>(gr, mr, vo, vm, {X(j, q)});")
+                w(f"                const float gyv_ = {_GY}<KIND>(gr, mr, vo, vm, {X(j, q)});")
                 w(f"                float suf_[{d + 1}];")
                 w(f"                suf_[{d}] = 0.f;")
                 for k in range(d - 1, -1, -1):
@@ -1299,7 +1312,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
                 w(f"        char* dg = stg_all + g * {4 * S.stage_floats};")
                 w(f"        for (int i = w0; i < NP; i += {S.threads}) {{")
                 w(f"            if (i + lane < NP) __builtin_amdgcn_raw_ptr_buffer_load_lds(sr, (lptr_t)(dg + i * {W_}), {W_}, "
-                  f"(uint32_t)(i + lane) * {W_}u, 0, 0, 0);")
+                  f"(uint32_t)(i + lane) * {W_}u, 0, 0, {2 if BWDCACHE >= 2 else 0});")
                 w("        }")
                 w("    }")
                 w("}")
@@ -1328,7 +1341,7 @@ def emit_bwd(S: Spec, ns: str = "fusedb") -> str:
         for j in S.reg_cols[p]:
             d = len(S.col_edges[j])
             for q in range(Q):
-                w(f"        {{ const float v_ = gy_masked<KIND>(gr, mr, vo, vm, {X(j, q)});")
+                w(f"        {{ const float v_ = {_GY}<KIND>(gr, mr, vo, vm, {X(j, q)});")
                 for k in range(d):
                     w(f"          g{q}[{s0 + k}] = v_;")
                 w("        }")

@@ -83,6 +83,14 @@ __device__ __forceinline__ void bstore8(rsrc_t r, uint32_t vo, int so, bool v) {
 __device__ __forceinline__ void bstore_i8(rsrc_t r, uint32_t vo, int so, int v) {
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v & 0xff), r, vo, so, 0);
 }
+// (r6, gen_fused.py NLDPC_GEN_FWDNT8, default on: the training forward's byte stores -- clamp masks, QMS saved codes --
+// non-temporal like its fp32 stores, so they do not evict the channel values the posteriors re-read)
+__device__ __forceinline__ void bstore8_nt(rsrc_t r, uint32_t vo, int so, bool v) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, vo, so, NLDPC_STORE_AUX);
+}
+__device__ __forceinline__ void bstore_i8_nt(rsrc_t r, uint32_t vo, int so, int v) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v & 0xff), r, vo, so, NLDPC_STORE_AUX);
+}
 // bytes per saved v2c message of a kernel kind (QMS saves int8 codes)
 template <int KIND>
 constexpr int saved_msg_bytes() { return KIND == NLDPC_QMS ? 1 : 4; }
@@ -435,6 +443,20 @@ __device__ __forceinline__ float gy_masked(rsrc_t gr, rsrc_t mr, uint32_t vo, ui
     const float g = bload(gr, vo, so);
     if (KIND == NLDPC_NEURAL) return g;
     return bload8(mr, vm, so >> 2) ? g : 0.f;
+}
+// r6 backward cache policy (gen_fused.py NLDPC_GEN_BWDCACHE, default on): streams read once per iteration loaded
+// non-temporal, so that they do not evict the VN-weight carry the next iteration reads back; the carry stored temporal
+__device__ __forceinline__ float bload_nt(rsrc_t r, uint32_t vo, int so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 2));
+}
+template <int KIND>
+__device__ __forceinline__ float gy_masked_nt(rsrc_t gr, rsrc_t mr, uint32_t vo, uint32_t vm, int so) {
+    const float g = bload_nt(gr, vo, so);
+    if (KIND == NLDPC_NEURAL) return g;
+    return __builtin_amdgcn_raw_buffer_load_b8(mr, vm, so >> 2, 2) ? g : 0.f;
+}
+__device__ __forceinline__ void bstore_keep(rsrc_t r, uint32_t vo, int so, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, vo, so, 0);
 }
 // Sum over the 64 lanes of a wave (wave-uniform result): DPP within rows of 16 (quad permutes, then the
 // half-row and row mirrors), then the gfx9 row broadcasts 15 / 31 carry the row sums up to lane 63,

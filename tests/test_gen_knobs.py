@@ -24,6 +24,8 @@ VARIANTS = [
     ("parts", {"NLDPC_GEN_PARTS": "1"}, ["fused_bg2_z16_s0.hip"]),
     # (r6 backward defaults off: the r5 read-backs and check node)
     ("bwd_r5", {"NLDPC_GEN_BWDPIPE": "0", "NLDPC_GEN_CNBSPARSE": "0", "NLDPC_GEN_KINDS": "2"}, ["fused_bg2_z16_bwd.hip"]),
+    ("cache_r5", {"NLDPC_GEN_BWDCACHE": "0", "NLDPC_GEN_FWDNT8": "0", "NLDPC_GEN_KINDS": "2"},
+     ["fused_bg2_z16_bwd.hip", "fused_bg2_z16_s1.hip"]),
     # (fetch bisect of the training forward, r6: the posteriors' channel re-reads replaced by registers)
     ("skip_xl", {"NLDPC_GEN_SKIP": "xlreg,xld1", "NLDPC_GEN_KINDS": "2", "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z16_s1.hip"]),
     # (UREMAT applies to one-codeword geometries: BG2 z=384's training forward; z=16 packs 16 codewords)
@@ -65,5 +67,5 @@ def test_no_pruned_knob_is_read():
     knobs = set(re.findall(r'environ\.get\("(NLDPC_[A-Z_0-9]+)"', src))
     assert knobs <= {"NLDPC_GEN_PARTS", "NLDPC_GEN_SKIP", "NLDPC_GEN_STAMPS", "NLDPC_GEN_GEOM", "NLDPC_GEN_WLATE",
                      "NLDPC_GEN_NOBWD", "NLDPC_GEN_ONLY", "NLDPC_GEN_KINDS", "NLDPC_FUSED_EXTRA", "NLDPC_GEN_UREMAT",
-                     "NLDPC_GEN_BWDPIPE", "NLDPC_GEN_CNBSPARSE"}, knobs
+                     "NLDPC_GEN_BWDPIPE", "NLDPC_GEN_CNBSPARSE", "NLDPC_GEN_BWDCACHE", "NLDPC_GEN_FWDNT8"}, knobs
     assert len(knobs) <= 15
