@@ -65,7 +65,9 @@ typedef struct nldpc_cfg {
 #define NLDPC_FLAG_FUSED 2       /* require the register-resident fused path (error if ineligible) */
 #define NLDPC_FLAG_NO_STATE 4    /* the caller does not need the final c2v state: c2v may be NULL
                                     when the fused path runs */
-#define NLDPC_FLAG_CN_TIED 8     /* (ABI 4, nldpc_backward) every row of w_cn repeats one weight (sharing code 3,
+#define NLDPC_FLAG_CN_TIED 8     /* (ABI 4, nldpc_backward; r6: also a saving nldpc_forward without UCN, which then runs
+                                    a kernel that reads one CN weight per iteration, w_cn[t][0]) every row of w_cn
+                                    repeats one weight (sharing code 3,
                                     BoostedNeuralLDPCDecoder.py:114-124): g_w_cn may receive each iteration's total
                                     in a few entries of its row and zeros elsewhere -- only row sums are meaningful,
                                     which is all a tied weight's gradient is.  The results (every gradient) are

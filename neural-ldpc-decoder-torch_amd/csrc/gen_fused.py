@@ -327,9 +327,13 @@ def emit(S: Spec) -> str:
     # MODE 0: decode, MODE 1: decode and save what the backward needs, MODE 2 / 3: count-only decode
     # (the posteriors are compared with the codeword and counted instead of stored):
     # 2 = all-zero codeword, decoder convention; 3 = either convention, against y when given
-    w("#define SAVE (MODE == 1)")
-    w("#define CNT (MODE >= 2)")
-    w("#define CM (MODE >= 2 ? MODE - 1 : 0)  // put_post: store / count / count against y")
+    # MODE 5 (r6): MODE 1 specialised for one CN weight per iteration (sharing code 3) and no UCN -- the tied saving
+    # forward fused_forward picks for NLDPC_FLAG_CN_TIED (FusedSpec::save_tied)
+    w("#define SAVE (MODE == 1 || MODE == 5)")
+    w("#define CNT (MODE == 2 || MODE == 3)")
+    w("#define CM (CNT ? MODE - 1 : 0)  // put_post: store / count / count against y")
+    w("#define TIEDW (MODE == 5)")
+    w("#define UCN_ON (!TIEDW && a.ucn)  // (the tied saving forward has no UCN code)")
     w("// check-row LDS addresses from one 32-bit base (ROADDR); in the QMS / SP kernels it measured slower")
     w("#define ROA (KIND == NLDPC_NEURAL || KIND == NLDPC_MS)")
     assert NZ < 65536  # per-codeword error counts are packed two to an LDS word
@@ -449,7 +453,7 @@ def emit(S: Spec) -> str:
               f"uint32_t vo, int it, rsrc_t pr, uint32_t vm, rsrc_t xr, rsrc_t pm, PostSink& ps, uint32_t* appw, int u, "
               f"rsrc_t apr) {{")
             if not final:
-                w("    const bool ucn_ = KIND != NLDPC_NEURAL && a.ucn;  // UCN: hard decisions of the previous posterior")
+                w("    const bool ucn_ = KIND != NLDPC_NEURAL && UCN_ON;  // UCN: hard decisions of the previous posterior")
             # every posterior's xa (cumulative VN weights) requested before the first posterior store: a later
             # load would wait (vmcnt counts loads and stores in order) for every store issued before it (XPRE)
             for n, j in enumerate(cols):
@@ -634,7 +638,7 @@ def emit(S: Spec) -> str:
                 w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{woff[i]} + k]; bv[k] = Bv[{woff[i]} + k]; }}")
                 w("        const bool wc = a.w_cn != nullptr;")
                 w("        float uf_ = 0.f;  // UCN: unsatisfied check (odd number of row variables with APP >= 0)")
-                w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
+                w("        if (KIND != NLDPC_NEURAL && UCN_ON) {")
                 w("            uint32_t par_ = 0;")
                 # every word of the row requested first, then the shifts and XORs (one LDS wait, not DC; UCNB)
                 ks = [(k, e) for k, e in enumerate(es) if e not in d1set]
@@ -658,7 +662,7 @@ def emit(S: Spec) -> str:
                 w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
                 w("        }")
                 if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
-                    w(f"        cn_copy<KIND, {DC}>(m{n}, wv, bv, a, wc, {i}, uf_);")
+                    w(f"        cn_copy<KIND, {DC}, TIEDW>(m{n}, wv, bv, a, wc, {i}, uf_);")
                 for k, e in enumerate(es):
                     if e in d1set:
                         j = int(S.hb_cols[e])
@@ -677,7 +681,7 @@ def emit(S: Spec) -> str:
                           f"y_ = posterior_m<KIND>(xo_, {pm}, a, m_); {_S8}(nm, (vo + dv_ + {4 * (j * Z + c)}u) >> 2, 0, m_); "
                           f"bstore(sxd, vo + dv_, {4 * (j * Z + c)}, cd[{ix}]); }}")
                         w(f"                else y_ = posterior<KIND>(xo_, {pm}, a);")
-                        w(f"                if (a.ucn) {bit_set('cdm', ix, 'y_ >= 0.f')};")
+                        w(f"                if (UCN_ON) {bit_set('cdm', ix, 'y_ >= 0.f')};")
                         w("            }")
                         if "d1post" in SKIP:  # (timing experiment: no degree-1 posterior stores)
                             w("            asm volatile(\"\" :: \"v\"(y_));")
@@ -742,7 +746,7 @@ def emit(S: Spec) -> str:
         remat = ("        if constexpr (SAVE) { u = ub + lane_id(); vo = 4u * (uint32_t)u; vc = vo; vm = (uint32_t)u; }"
                  if S.uremat else None)
         if S.pipe:  # (r2: the pipelined schedule made the training forward slower; r5 with the check-node saves: still)
-            w("    static_assert(MODE != 1, \"the SAVE kernels use the one-buffer schedule\");")
+            w("    static_assert(!SAVE, \"the SAVE kernels use the one-buffer schedule\");")
         for i in range(Q):
             w(f"    float cs{i}[{sp}], xs{i}[{nr}];")
         w("#pragma unroll")
@@ -795,7 +799,7 @@ def emit(S: Spec) -> str:
         # iteration's array is cleared in the read-back phase of the iteration before
         w(f"    uint32_t cdm[{nwords(p)}] = {{}};  // UCN: hard decisions of the posteriors of its cd entries")
         w(f"    const rsrc_t apr = make_rsrc(a.app_prev ? a.app_prev + blk * {NZ} : a.xa, a.app_prev ? nlive * {4 * NZ} : 0);")
-        w("    if (KIND != NLDPC_NEURAL && a.ucn) {")
+        w("    if (KIND != NLDPC_NEURAL && UCN_ON) {")
         w(f"        for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
         w("        __syncthreads();")
         w("    }")
@@ -846,7 +850,7 @@ def emit(S: Spec) -> str:
             # at the start of the check-node phase (WLATE)
             w("        {")
             w("            const cfloat_p wc_ = a.w_cn ? (cfloat_p)(a.w_cn + (int64_t)it * E) : nullptr;")
-            w("            const float* bsrc_ = KIND == NLDPC_NEURAL ? a.bias : (a.ucn ? a.w_ucn : nullptr);  // bias / UCN weight")
+            w("            const float* bsrc_ = KIND == NLDPC_NEURAL ? a.bias : (UCN_ON ? a.w_ucn : nullptr);  // bias / UCN weight")
             w("            const cfloat_p bs_ = bsrc_ ? (cfloat_p)(bsrc_ + (int64_t)it * E) : nullptr;")
             wo, wl, bl = 0, [], []
             for i in S.cn_order[(p, ci)]:
@@ -854,6 +858,10 @@ def emit(S: Spec) -> str:
                     wl.append(f"W{ci}[{wo}] = wc_[{e}];")
                     bl.append(f"B{ci}[{wo}] = bs_[{e}];")
                     wo += 1
+            w("            if constexpr (TIEDW) {  // one CN weight per iteration: the row's first entry, one scalar")
+            w("                const float w0_ = wc_ ? wc_[0] : 1.f;")
+            w(f"                for (int k = 0; k < {nw}; ++k) {{ W{ci}[k] = w0_; B{ci}[k] = 0.f; }}")
+            w("            } else {")
             if "wload" in SKIP:  # timing experiment only: constant weights, no scalar loads
                 w(f"            for (int k = 0; k < {nw}; ++k) {{ W{ci}[k] = 0.5f; B{ci}[k] = 0.f; }}")
             else:
@@ -861,6 +869,7 @@ def emit(S: Spec) -> str:
                 w(f"            else {{ for (int k = 0; k < {nw}; ++k) W{ci}[k] = 1.f; }}")
                 w(f"            if (KIND == NLDPC_NEURAL || bs_) {{ {' '.join(bl)} }}")
                 w(f"            else {{ for (int k = 0; k < {nw}; ++k) B{ci}[k] = 0.f; }}")
+            w("            }")
             w("        }")
 
         def buf(ci):
@@ -888,7 +897,7 @@ def emit(S: Spec) -> str:
             w(f"        rd_p{p}_c{ci}<KIND, MODE>({state_args(p)}, {x_args(p)}, {buf(ci)}, u, a, vo, nr, cr, vc, co_last, vm, xr, nm, "
               f"ps);")
             if ci == len(S.chunks) - 1:  # every check node of the iteration has read the bits
-                w("        if (KIND != NLDPC_NEURAL && a.ucn) {")
+                w("        if (KIND != NLDPC_NEURAL && UCN_ON) {")
                 w(f"            for (int i_ = threadIdx.x; i_ < {S.G_lds * S.N * S.WZX}; i_ += {S.threads}) app_all[i_] = 0u;")
                 w("        }")
 
@@ -922,7 +931,7 @@ def emit(S: Spec) -> str:
             if K % 2 == 1:
                 w("        __syncthreads();")
             else:  # UCN: the bits cleared in R_{K-1} must be clear before any wave's next VN
-                w("        if (KIND != NLDPC_NEURAL && a.ucn) __syncthreads();")
+                w("        if (KIND != NLDPC_NEURAL && UCN_ON) __syncthreads();")
         w("    }")
         w("    const float* pl = a.outs.p[a.T - 1];")
         w(f"    const rsrc_t lr = make_rsrc(pl ? pl + blk * {NZ} : a.xa, pl ? nlive * {4 * NZ} : 0);")
@@ -985,6 +994,8 @@ def emit(S: Spec) -> str:
     w("#undef SAVE")
     w("#undef CNT")
     w("#undef CM")
+    w("#undef TIEDW")
+    w("#undef UCN_ON")
     w("}  // namespace")
     return "\n".join(L)
 
@@ -1545,6 +1556,14 @@ def main():
                     src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, {save}>);")
             src.append("    return nullptr;")
             src.append("}")
+            if save == 1:  # (r6) the tied saving forward, MODE 5, Boosted MS / QMS
+                src.append(f"void* fused_{S.tag}_kernel_s1t(int kind) {{")
+                if on:
+                    for k in kinds:
+                        if k in (1, 2):
+                            src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, 5>);")
+                src.append("    return nullptr;")
+                src.append("}")
             src.append("}  // namespace nldpc")
             write(f"fused_{S.tag}_s{save}.hip", src)
         # backward kernels: the fp32-message kinds and QMS (int8 codes) stage their saved messages in LDS
@@ -1579,6 +1598,7 @@ def main():
             src.append(f"void* fused_{S.tag}_kernel_s{v}(int kind);")
         src.append(f"void* fused_{S.tag}_bwd(int kind);")
         src.append(f"void* fused_{S.tag}_bwd_tied(int kind);")
+        src.append(f"void* fused_{S.tag}_kernel_s1t(int kind);")
         for v in MODES:
             src.append(f"uint32_t fused_{S.tag}_sig_s{v}();")
         src.append(f"uint32_t fused_{S.tag}_sig_bwd();")
@@ -1591,8 +1611,9 @@ def main():
         kb = ", ".join(f"fused_{S.tag}_bwd({k})" for k in range(4))
         kt = ", ".join(f"fused_{S.tag}_bwd_tied({k})" for k in range(4))
         sg = ", ".join([f"fused_{S.tag}_sig_s{v}()" for v in MODES] + [f"fused_{S.tag}_sig_bwd()"] * 2)
+        st = ", ".join(f"fused_{S.tag}_kernel_s1t({k})" for k in range(4))
         src.append(f"        {{\"{S.tag}\", {S.M}, {S.N}, {S.Z}, {S.E}, {S.G}, {S.threads}, basegraph_{S.tag}, "
-                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}, {{{kt}}}, {{{sg}}}}},")
+                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}, {{{kt}}}, {{{sg}}}, {{{st}}}}},")
     src.append("    };")
     src.append(f"    *n = {len(specs)};")
     src.append("    return tab;")

@@ -292,7 +292,13 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
                          float* const* outs, const float* app_prev, float* c2v, void* saved, hipStream_t s,
                          const uint8_t* cnt_y = nullptr, int32_t cnt_conv = 0, int64_t* counts = nullptr) {
     const int mode = saved ? 1 : (counts ? ((cnt_y || cnt_conv) ? 3 : 2) : 0);
-    const FusedLaunch f = fused_launch(g, mode, cfg->kind);
+    // (r6) a saving forward with one CN weight per iteration (NLDPC_FLAG_CN_TIED: sharing code 3, cfg5's NW(3,0,3)) and no
+    // UCN runs the kernel specialised for it when the library has one: one scalar weight per iteration instead of a
+    // per-edge row in SGPRs (the per-edge kernel spilled ~1 450 SGPRs), the UCN code not compiled
+    const bool tied = saved && (cfg->flags & NLDPC_FLAG_CN_TIED) && w_cn && !cfg->ucn &&
+                      (cfg->kind == NLDPC_MS || cfg->kind == NLDPC_QMS);
+    const FusedLaunch ft = tied ? fused_launch(g, 6, cfg->kind) : FusedLaunch{};
+    const FusedLaunch f = ft ? ft : fused_launch(g, mode, cfg->kind);
     if (!f) return fail(NLDPC_EUNSUPPORTED, "no register-resident kernel for this graph / mode / kind");
     FusedArgs fa{};
     fa.sig = kFusedArgsSig;

@@ -609,7 +609,8 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
 // check node of one check copy in place (m: gathered v2c -> c2v), every kind: Neural through the
 // specialised neural_row, MS / QMS through boosted_row, SP through the shared cn_core + cn_epilogue
 // bv: Neural biases, or (Boosted with UCN) the UCN weights; uf: the copy's UCN flag
-template <int KIND, int DC>
+// NOUCN: the kernel variant without UCN (the tied saving forward, MODE 5): the UCN branch is not compiled
+template <int KIND, int DC, bool NOUCN = false>
 __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], const float (&bv)[DC],
                                         const FusedArgs& a, bool has_w, int row, float uf) {
     if constexpr (KIND == NLDPC_NEURAL) {
@@ -617,7 +618,7 @@ __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], c
     } else if constexpr (KIND == NLDPC_MS || KIND == NLDPC_QMS) {
         // QMS reaches the fused kernels only with an active quantiser (fused_eligible): the generic
         // cn_core is not compiled into them (it had made the QMS kernels 6x the code of the MS ones)
-        boosted_row<DC, KIND>(m, wv, has_w, a.qp, a.lo, a.hi, a.ucn != 0, uf, bv);
+        boosted_row<DC, KIND>(m, wv, has_w, a.qp, a.lo, a.hi, !NOUCN && a.ucn != 0, uf, bv);
     } else {
         CnCore<DC> core;
         cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core, SpRow{a.sp_plan + row * kSpPlanBytes, a.tanh});
@@ -643,12 +644,15 @@ struct FusedSpec {
     void* bwd_tied[4];         // backward kernels for tied CN / VN weights (MODE 5 in fused_launch), or nullptr
     uint32_t sig[6];           // the argument layout each MODE's unit was built for (kFusedArgsSig / kFusedBwdArgsSig):
                                // fused_launch refuses a kernel whose layout differs from the launcher's
+    void* save_tied[4];        // (r6) saving forward for one CN weight per iteration and no UCN (MODE 6 in fused_launch;
+                               // the generated kernel<KIND, 5>), or nullptr; built in the saving unit (sig[1])
 };
 
 const FusedSpec* fused_specs(int* n);
 
 // How to launch the register-resident kernel of (graph, MODE, kind) (MODE 4: the backward; MODE 5: the
-// backward for tied weights, library kernels only -- a run-time compiled graph uses MODE 4): one compiled
+// backward for tied weights; MODE 6: the saving forward for tied CN weights without UCN -- MODES 5 and 6 library
+// kernels only, a run-time compiled graph uses MODE 4 / 1): one compiled
 // into the library (fused_specs table, hipLaunchKernel) or one compiled at run time for this graph and
 // attached (nldpc_graph_attach_kernel, hipModuleLaunchKernel); empty when neither exists.
 struct FusedLaunch {

@@ -65,6 +65,7 @@ def decode(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *, w_cn
     Returns (outputs [T, B, N*Z], c2v state [B, E, Z], saved byte buffer for the backward or None).
     c2v: optional incoming state [B, E, Z] (None = all-zero messages)."""
     _require_device_tensor(xa, "xa")
+    cfg = _honour_tied(cfg, w_cn)  # (r6: the tied flag also selects the tied saving forward)
     if xa.dim() != 3 or xa.shape[1] != graph.N or xa.shape[2] != graph.Z:
         raise ValueError(f"xa must be [B, {graph.N}, {graph.Z}], got {tuple(xa.shape)}")
     dev = xa.device
@@ -114,6 +115,7 @@ def decode_count(graph: LiftedGraph, cfg: DecodeCfg, xa: torch.Tensor, T: int, *
     without a compiled kernel, UCN resumed at first_iter > 0) run decode + the device counter instead
     (both on the device); app_prev: the posterior of iteration first_iter - 1 for those UCN calls."""
     _require_device_tensor(xa, "xa")
+    cfg = _honour_tied(cfg, w_cn)  # (r6: the tied flag also selects the tied saving forward)
     if xa.dim() != 3 or xa.shape[1] != graph.N or xa.shape[2] != graph.Z:
         raise ValueError(f"xa must be [B, {graph.N}, {graph.Z}], got {tuple(xa.shape)}")
     dev = xa.device
