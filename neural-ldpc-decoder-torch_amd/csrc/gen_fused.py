@@ -708,8 +708,9 @@ def emit(S: Spec) -> str:
 
     # ---------------------------------------------------------------- the kernel
     def each_part(fmt, indent="        "):
-        for p in PARTS or range(S.P):
-            w(f"{indent}{'if' if p == 0 else 'else if'} (p == {p}) {fmt.format(p=p)};")
+        ps_ = list(PARTS or range(S.P))
+        for p in ps_:
+            w(f"{indent}{'if' if p == ps_[0] else 'else if'} (p == {p}) {fmt.format(p=p)};")
 
     # Each part runs its own copy of the whole iteration loop: its register state never meets another
     # part's at a control-flow join (per-phase part branches inside one loop made the register

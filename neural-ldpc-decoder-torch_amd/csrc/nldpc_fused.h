@@ -101,7 +101,18 @@ constexpr int saved_msg_bytes() { return KIND == NLDPC_QMS ? 1 : 4; }
 // QMS quantiser of the channel values and posteriors in the fused kernels
 // (the generic quantize(): the four-operation quantize_active behind a select measured 15 % slower in the
 // fused QMS kernels, cfg3 NW(1,1,2) 187.6 -> 217 ms -- register allocation, not operation count)
-__device__ __forceinline__ float qms_q(float x, const QParams& p) { return quantize_p(x, p); }
+// r6 (NLDPC_QFAST, default): quantize_active_p's four operations with the last multiply as fma(., inv, +0) -- the
+// reference's STE form never returns -0 (xc + (qv - xc) rounds an exact cancellation to +0), and the +0 addend
+// makes the zeros agree too: equal to quantize_p bit for bit for every non-NaN x (tests/test_qms_code.py), where
+// quantize_p spends two compare-and-select clamps (four v_cmp, 5.2 cycles each) on NaN propagation.  A NaN channel
+// value gives -hi here instead of NaN.
+__device__ __forceinline__ float qms_q(float x, const QParams& p) {
+#if NLDPC_QFAST
+    return __builtin_fmaf(__builtin_amdgcn_fmed3f(rintf(fmul(x, p.s)), -p.hs, p.hs), p.inv, 0.f);
+#else
+    return quantize_p(x, p);
+#endif
+}
 
 template <int KIND>
 __device__ __forceinline__ float chan(float x, const FusedArgs& a) {
@@ -128,8 +139,16 @@ template <int KIND>
 __device__ __forceinline__ float posterior_m(float xav, float P, const FusedArgs& a, bool& m) {
     const float xo = (KIND == NLDPC_QMS) ? qms_q(xav, a.qp) : xav;
     const float yp = fadd(xo, P);
+#if NLDPC_QFAST
+    // (r6) the clamp as one med3 and the mask as "the clamp changed nothing": one v_cmp instead of four and two
+    // selects; the same for every non-NaN sum (lo <= hi); NaN: mask 0 as before, the value lo instead of NaN
+    const float y = __builtin_amdgcn_fmed3f(yp, a.lo, a.hi);
+    m = y == yp;
+    return y;
+#else
     m = yp >= a.lo && yp <= a.hi;
     return clampf(yp, a.lo, a.hi);
+#endif
 }
 
 // v2c of a degree-1 edge from the channel value its check-node thread holds (degree-1 bypass): Neural

@@ -118,11 +118,29 @@ __device__ __forceinline__ int qms_code(float m, int q) {
     return (int)c;
 }
 // qms_code() for an active q with the constants given (2 / s = 2 inv)
+// NLDPC_QFAST (default; r6): no compare or select.  With u = m s (exact), cl = med3(u, +-hi s) and w = u - cl (0
+// inside the clip range, of the sign of m and at least one ulp of hi s outside it): w * 2^30 + med3(rint(u), +-hi s)
+// is the in-range value inside the range and beyond (hi + 1) s outside it, so one more med3 at +-(hi + 1) s gives
+// the code / (2/s) in both cases.  (rint before the clip, as quantize_active: q = 6's hi s = 15.5 is not an integer.)  NaN: v_med3_f32 with a NaN operand returns the minimum of the other two (the gfx9 ISA definition,
+// also LLVM's constant folding of llvm.amdgcn.fmed3), so cl = -hi s, c = NaN and the code -(2 hi + 2), as defined.
+// (tests/test_qms_code.py models both forms.)
+#ifndef NLDPC_QFAST
+#define NLDPC_QFAST 1
+#endif
 __device__ __forceinline__ int qms_code_p(float m, const QParams& p) {
+#if NLDPC_QFAST
+    const float u = fmul(m, p.s);
+    const float cl = __builtin_amdgcn_fmed3f(u, -p.hs, p.hs);
+    const float r = __builtin_amdgcn_fmed3f(rintf(u), -p.hs, p.hs);
+    const float c = __builtin_fmaf(__fsub_rn(u, cl), 1073741824.f, r);
+    const float co = p.hs + p.s;  // (hi + 1) s
+    return (int)fmul(__builtin_amdgcn_fmed3f(c, -co, co), 2.f * p.inv);
+#else
     const float c_out = 2.f * p.hi + 2.f;
     const float t = fmul(__builtin_amdgcn_fmed3f(rintf(fmul(m, p.s)), -p.hs, p.hs), 2.f * p.inv);
     const float c = fabsf(m) <= p.hi ? t : (m > 0.f ? c_out : -c_out);
     return (int)c;
+#endif
 }
 __device__ __forceinline__ float qms_decode(int c) { return 0.5f * (float)c; }
 

@@ -1,8 +1,8 @@
 #!/bin/bash
 # The ISA instruction budget of a generated fused kernel (tools/isa_budget.py): one single-part build per part (gfx950
 # asm, hipcc -S, CPU only, about a minute per part, parts in parallel), the kernel's hot loop per part, VALU issue cycles.
-# Usage: [TAG=bg2_z384] [UNIT=s0|s1|s2|s3|bwd] [KIND=3] [TIED=0|1] [ISA_JSON=profiles/isa_budget.json] bash tools/isa_budget.sh [OUTDIR]
-#   UNIT s<MODE>: the forward kernel<KIND, MODE>; bwd: the backward bwd_kernel<KIND, TIED>.  Default: the cfg3 decode kernel.
+# Usage: [TAG=bg2_z384] [UNIT=s0|s1|s2|s3|bwd] [MODE=<kernel MODE, default the unit's>] [KIND=3] [TIED=0|1] [ISA_JSON=profiles/isa_budget.json] bash tools/isa_budget.sh [OUTDIR]
+#   UNIT s<MODE>: the forward kernel<KIND, MODE> (MODE=5 with UNIT=s1: the tied saving forward); bwd: the backward bwd_kernel<KIND, TIED>.  Default: the cfg3 decode kernel.
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 CS=$ROOT/neural-ldpc-decoder-torch_amd/csrc
@@ -27,6 +27,6 @@ for p in $(seq 0 $((P - 1))); do
 done
 wait
 if [ "$UNIT" = bwd ]; then FUNC="bwd_kernelILi${KIND}ELi${TIED}E"; NAME="_bg2_z384::bwd_kernel<${KIND}, ${TIED}>"; NAME="${TAG}::bwd_kernel<${KIND}, ${TIED}>";
-else M=${UNIT#s}; FUNC="kernelILi${KIND}ELi${M}E"; NAME="fused_${TAG}::kernel<${KIND}, ${M}>"; fi
+else M=${MODE:-${UNIT#s}}; FUNC="kernelILi${KIND}ELi${M}E"; NAME="fused_${TAG}::kernel<${KIND}, ${M}>"; fi
 python3 "$ROOT/tools/isa_budget.py" --func="$FUNC" --name="$NAME" --geom="$G,$P,$WPP,$THREADS" ${ISA_JSON:+--json=$ISA_JSON} \
   $(for p in $(seq 0 $((P - 1))); do echo "$OUT/parts/p$p.s"; done)
