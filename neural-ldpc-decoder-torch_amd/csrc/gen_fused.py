@@ -657,8 +657,9 @@ def emit(S: Spec) -> str:
                     j = int(S.hb_cols[e])
                     # the hard decision of this thread's own previous posterior of that edge's column copy
                     ix = S.cd_index[p].index((e, q))
-                    app0 = f"(a.first_iter > 0 ? bload(apr, vo + {dvu}, {4 * (j * Z + c)}) : chan<KIND>(cd[{ix}], a))"
-                    w(f"            par_ ^= it == 0 ? ({app0} >= 0.f ? 1u : 0u) : {bit_get('cdm', ix)};")
+                    # (r6: iteration 0's bits -- APP = xa_input or the previous call's posterior -- are set into cdm at
+                    # the top of iteration 0, run_p: no per-iteration select between the two sources)
+                    w(f"            par_ ^= {bit_get('cdm', ix)};")
                 w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
                 w("        }")
                 if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
@@ -816,6 +817,16 @@ def emit(S: Spec) -> str:
                 w(f"                bstore(sx, vo, {X(j, q)}, {xref(p, j, q)});")
         w("            }")
         w("        }")
+        # UCN, iteration 0: the degree-1 entries' hard decisions of APP = xa_input (after this iteration's VN-weight step)
+        # or of the previous call's posterior, into cdm once (the check nodes read cdm in every iteration)
+        if S.cd_index[p]:
+            w("        if (KIND != NLDPC_NEURAL && UCN_ON && it == 0) {")
+            for ix, (e, q) in enumerate(S.cd_index[p]):
+                j = int(S.hb_cols[e])
+                c, dvu = rot(e, q)
+                app0 = f"(a.first_iter > 0 ? bload(apr, vo + {dvu}, {4 * (j * Z + c)}) : chan<KIND>(cd[{ix}], a))"
+                w(f"            {bit_set('cdm', ix, app0 + ' >= 0.f')};")
+            w("        }")
         # (the check-node threads store the degree-1 columns' xin: cn_p)
         w("        float* sxd_ = (SAVE && KIND != NLDPC_NEURAL && a.w_vn && a.sxin) ? a.sxin + it * a.sxin_stride : nullptr;")
         w(f"        const rsrc_t sxd = make_rsrc(sxd_ ? sxd_ + blk * {NZ} : a.xa, sxd_ ? nlive * {4 * NZ} : 0);")

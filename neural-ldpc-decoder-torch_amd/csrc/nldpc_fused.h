@@ -571,7 +571,13 @@ __device__ __forceinline__ void boosted_row_keys(float (&m)[DC], const float (&w
 // the reference's (|x| w)(1 - u) + (|x| w_u) u is exactly |x| w or |x| w_u (a select).  DC == 1 rows
 // (the masked 10000 would be the magnitude) keep the key form.  Equal to boosted_row_keys up to the
 // sign bit of a zero c2v, which no sum of the decoder observes.
-template <int DC, int KIND>
+// TIED (the tied saving forward, MODE 5: one CN weight per row, w[k] == w[0], 1.f without weights, no UCN): every edge's
+// epilogue is one of two values -- the magnitudes mg1 / mg2 times the one weight, clipped or quantised -- computed once
+// per row copy from the same operands (bit-identical), so an edge costs the two selects only (r6).
+#ifndef NLDPC_TIEDROW
+#define NLDPC_TIEDROW 1
+#endif
+template <int DC, int KIND, bool TIED = false>
 __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC], bool has_w, const QParams& qp, float lo,
                                             float hi, bool ucn, float uf, const float (&wu)[DC]) {
     if constexpr (DC >= 2) {
@@ -608,12 +614,31 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
                 pos[k] = KIND == NLDPC_MS ? m[k] > 0.f : m[k] >= thr;
                 par ^= pos[k];
             }
+            if constexpr (TIED && NLDPC_TIEDROW) {
+                // (w[0] is 1.f without weights: mag * 1 == mag, the !has_w value)
+                auto epi = [&](float mag) {
+                    const float x1 = fmul(mag, w[0]);
+                    return KIND == NLDPC_MS ? __builtin_amdgcn_fmed3f(x1, lo0, top)
+                                            : fmul(__builtin_amdgcn_fmed3f(rintf(x1), 0.f, top), inv);
+                };
+                const float x3a = epi(mg1), x3b = epi(mg2);
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    const float x3 = fabsf(m[k]) == min1 ? x3b : x3a;
+                    m[k] = (par != pos[k]) ? x3 : -x3;
+                }
+                return;
+            }
+            // (r6) the weights are 1.f without a CN weight (the kernels' preload), and mag * 1 == mag: no per-edge select of
+            // the unweighted value; the UCN weight only with CN weights (the reference's CN sharing 0 ignores UCN)
+            const bool uw = ucn && has_w && uf != 0.f;
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
                 const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
                 // (a wave-uniform branch to the plain weights when no copy is unsatisfied, i.e. two versions
                 // of this loop, measured 15 % slower: code size)
-                const float x1 = !has_w ? mag : fmul(mag, (ucn && uf != 0.f) ? wu[k] : w[k]);
+                const float x1 = NLDPC_TIEDROW ? fmul(mag, uw ? wu[k] : w[k])
+                                               : (!has_w ? mag : fmul(mag, (ucn && uf != 0.f) ? wu[k] : w[k]));
                 float x3;
                 if constexpr (KIND == NLDPC_MS) x3 = __builtin_amdgcn_fmed3f(x1, lo0, top);
                 else x3 = fmul(__builtin_amdgcn_fmed3f(rintf(x1), 0.f, top), inv);
@@ -628,7 +653,8 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
 // check node of one check copy in place (m: gathered v2c -> c2v), every kind: Neural through the
 // specialised neural_row, MS / QMS through boosted_row, SP through the shared cn_core + cn_epilogue
 // bv: Neural biases, or (Boosted with UCN) the UCN weights; uf: the copy's UCN flag
-// NOUCN: the kernel variant without UCN (the tied saving forward, MODE 5): the UCN branch is not compiled
+// NOUCN: the kernel variant without UCN and with one CN weight per row (the tied saving forward, MODE 5): the UCN
+// branch is not compiled and the row's epilogue is computed once (boosted_row TIED)
 template <int KIND, int DC, bool NOUCN = false>
 __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], const float (&bv)[DC],
                                         const FusedArgs& a, bool has_w, int row, float uf) {
@@ -637,7 +663,7 @@ __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], c
     } else if constexpr (KIND == NLDPC_MS || KIND == NLDPC_QMS) {
         // QMS reaches the fused kernels only with an active quantiser (fused_eligible): the generic
         // cn_core is not compiled into them (it had made the QMS kernels 6x the code of the MS ones)
-        boosted_row<DC, KIND>(m, wv, has_w, a.qp, a.lo, a.hi, !NOUCN && a.ucn != 0, uf, bv);
+        boosted_row<DC, KIND, NOUCN>(m, wv, has_w, a.qp, a.lo, a.hi, !NOUCN && a.ucn != 0, uf, bv);
     } else {
         CnCore<DC> core;
         cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core, SpRow{a.sp_plan + row * kSpPlanBytes, a.tanh});

@@ -117,7 +117,7 @@ __device__ __forceinline__ int qms_code(float m, int q) {
     const float c = fabsf(m) <= r.hi ? t : (m > 0.f ? c_out : -c_out);
     return (int)c;
 }
-// qms_code() for an active q with the constants given (2 / s = 2 inv)
+// qms_code() for an active q with the constants given (2 / s = 2 inv); NLDPC_QFAST: the code modulo 256 (byte stores)
 // NLDPC_QFAST (default; r6): no compare or select.  With u = m s (exact), cl = med3(u, +-hi s) and w = u - cl (0
 // inside the clip range, of the sign of m and at least one ulp of hi s outside it): w * 2^30 + med3(rint(u), +-hi s)
 // is the in-range value inside the range and beyond (hi + 1) s outside it, so one more med3 at +-(hi + 1) s gives
@@ -134,7 +134,10 @@ __device__ __forceinline__ int qms_code_p(float m, const QParams& p) {
     const float r = __builtin_amdgcn_fmed3f(rintf(u), -p.hs, p.hs);
     const float c = __builtin_fmaf(__fsub_rn(u, cl), 1073741824.f, r);
     const float co = p.hs + p.s;  // (hi + 1) s
-    return (int)fmul(__builtin_amdgcn_fmed3f(c, -co, co), 2.f * p.inv);
+    // the conversion to an integer as an add of 1.5 * 2^23 folded into the scaling: the code k (|k| <= 33) is exact in
+    // the low mantissa bits of 1.5 * 2^23 + k, whose low byte is k's two's complement -- all the byte store keeps
+    // (no v_cvt_i32_f32; the returned int is the code only modulo 256)
+    return __builtin_bit_cast(int, __builtin_fmaf(__builtin_amdgcn_fmed3f(c, -co, co), 2.f * p.inv, 12582912.f));
 #else
     const float c_out = 2.f * p.hi + 2.f;
     const float t = fmul(__builtin_amdgcn_fmed3f(rintf(fmul(m, p.s)), -p.hs, p.hs), 2.f * p.inv);

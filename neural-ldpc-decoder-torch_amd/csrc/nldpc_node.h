@@ -16,6 +16,9 @@
 #ifndef NLDPC_CNB_SPARSE
 #define NLDPC_CNB_SPARSE 0
 #endif
+#ifndef NLDPC_CNB_P2  // (r6) the tied QMS check node's folded pass 2 (cn_bwd_ms)
+#define NLDPC_CNB_P2 1
+#endif
 
 namespace nldpc {
 
@@ -494,13 +497,47 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
     // r6 (gen_fused.py NLDPC_GEN_CNBSPARSE): the tied kernel's check node with fewer VALU (below); the untied kernel
     // keeps the r5 form (the same edits there spilled 204 VGPRs)
     constexpr bool kSparse = NLDPC_CNB_SPARSE && SAMEW;
-    if constexpr (kSparse && KIND == NLDPC_QMS && DC >= 2 && DC <= 16) {
+    constexpr bool kKeys = kSparse && KIND == NLDPC_QMS && DC >= 2 && DC <= 16;
+    // (r6, NLDPC_CNB_P2) key bits below the index: the sign and the STE mask of the edge, so that pass 3 reads the two
+    // argmins' own from their keys; every code value's float has its low 17 mantissa bits clear
+    constexpr bool kP2 = kKeys && NLDPC_CNB_P2;
+    uint32_t ka = 0, kb = 0;
+    if constexpr (kP2) {
+        // pass 1: key = max(bits(|xc|), bits(1e-4) & ~63) | k << 2 | neg << 1 | ok -- the zero fix as the max (every
+        // nonzero |xc| >= 0.5), the sign from xd's sign bit (a decoded code is never -0, and the clamp and the zero fix
+        // keep it), the mask as clamp(x) == x; the ordering by (|x|, k) is the r6 key's
+        constexpr uint32_t kZk = 0x38D1B717u & ~63u;
+        static_assert(__builtin_bit_cast(uint32_t, kZeroFix) == 0x38D1B717u, "zero-fix constant");
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const float xd = load_m(k);
+            const float xc = __builtin_amdgcn_fmed3f(xd, qr.lo, qr.hi);
+            const uint32_t ok = xc == xd;
+            const uint32_t neg = __builtin_bit_cast(uint32_t, xd) >> 31;
+            negm |= neg << k;
+            const uint32_t key = max(__builtin_bit_cast(uint32_t, xc) & 0x7FFFFFFFu, kZk) | ((uint32_t)k << 2) | (neg << 1) | ok;
+            if (k == 0) {
+                ka = key;
+            } else if (k == 1) {
+                kb = max(ka, key);
+                ka = min(ka, key);
+            } else {
+                asm("v_med3_u32 %0, %1, %2, %3" : "=v"(kb) : "v"(ka), "v"(kb), "v"(key));
+                ka = min(ka, key);
+            }
+        }
+        posm = ~negm & ((1u << DC) - 1u);
+        npos = (uint32_t)__builtin_popcount(posm) & 1u;
+        idx1 = (int)((ka >> 2) & 15u);
+        idx2 = (int)((kb >> 2) & 15u);
+        min1 = (ka & ~63u) == kZk ? kZeroFix : __builtin_bit_cast(float, ka & ~63u);
+        min2 = (kb & ~63u) == kZk ? kZeroFix : __builtin_bit_cast(float, kb & ~63u);
+    } else if constexpr (kKeys) {
         // (r6) QMS pass 1 on ordering keys: every conditioned input is a decoded int8 code (a multiple of 0.5 below 17,
         // a few mantissa bits) or the zero fix 1e-4, so (bits(|x|) & ~15) | k orders the edges by |x| with the first
         // index winning ties -- torch.min's argmin -- and the two smallest keys (v_min_u32 / v_med3_u32, two ops per
         // edge) give both minima and both indices: no compare-and-select chain per edge.  The STE mask as one compare
         // (clamp(x) == x), x never 0 after the zero fix so x < 0 is !(x > 0).  Bit-identical inputs to passes 2 and 3.
-        uint32_t ka = 0, kb = 0;
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
             const float xd = load_m(k);
@@ -575,7 +612,34 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
     }
     }
     float g_at1 = 0.f, g_at2 = 0.f;
-    if constexpr (SAMEW && KIND != NLDPC_NEURAL) {
+    if constexpr (kP2) {
+        // (r6) the tied QMS check node's pass 2 with the per-row constants folded: the masks mA / mB are 0 or 1, so
+        // ((gc s) m) |mag| == (gc s)(m |mag|) and ((gc s) m) w == (gc s)(m w) up to the sign of a zero (every sum here
+        // starts from +0); s = +-1 is a sign flip of gc (bit k of R: s_k = -1), no compare or multiply; the first-index
+        // argmin's own term (g_at2) once per row from its LDS slot instead of a select per edge, and its g_at1 term a
+        // +0.  The same sums in the same order, bit for bit, for finite gradients (profiles/r6_ab_cnb_p2.txt).
+        const float magA = (min1 > kZeroFix) ? min1 : fadd(min1, -kZeroFix);
+        const float magB = (min2 > kZeroFix) ? min2 : fadd(min2, -kZeroFix);
+        const float x1A = has_w ? fmul(fabsf(magA), wc[0]) : fabsf(magA);
+        const float x1B = has_w ? fmul(fabsf(magB), wc[0]) : fabsf(magB);
+        // (x1 > 0 ? in_range(relu(x1), lo, hi) : 0) with lo < 0: x1 in (0, hi] (NaN: 0, as before)
+        const float mA = (x1A > 0.f && (!qr.active || x1A <= qr.hi)) ? 1.f : 0.f;
+        const float mB = (x1B > 0.f && (!qr.active || x1B <= qr.hi)) ? 1.f : 0.f;
+        const float PA = fmul(mA, fabsf(magA)), PB = fmul(mB, fabsf(magB));
+        const float QA = has_w ? fmul(mA, wc[0]) : mA, QB = has_w ? fmul(mB, wc[0]) : mB;
+        const uint32_t R = ~(posm ^ (0u - (npos & 1u)));
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const bool sel = k == idx1;
+            const float gcs = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, lds[k * stride]) ^
+                                                            ((R << (31 - k)) & 0x80000000u));
+            if (has_w) gwa[0] += gcs * (sel ? PB : PA);
+            g_at1 += gcs * (sel ? 0.f : QA);
+        }
+        const float gc1 = lds[idx1 * stride];
+        const float gcs1 = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, gc1) ^ (((R >> idx1) & 1u) << 31));
+        g_at2 = fadd(0.f, gcs1 * QB);
+    } else if constexpr (SAMEW && KIND != NLDPC_NEURAL) {
         // A: every edge but idx1 (magnitude min1), B: edge idx1 (min2); the zero-fix correction, x1 = |x| w
         // (|x| = |mag|: x = mag * (+-1)), the clip / quantiser mask of relu(x1) and the relu mask, per row
         const float magA = (min1 > kZeroFix) ? min1 : fadd(min1, -kZeroFix);
@@ -657,6 +721,17 @@ __device__ __forceinline__ void cn_bwd_ms(LoadM&& load_m, float* lds, int stride
     // started from +0: the owners' VN backward and the degree-1 chains)
 #pragma unroll
     for (int l = 0; l < DC; ++l) lds[l * stride] = 0.f;
+    if constexpr (kP2) {
+        // (r6) the argmins' sign and mask from their keys: (gl * (+-1)) * msk as a sign flip and a select (a zero of
+        // either sign for a masked edge, as the dense form's product -- every consumer's sum starts from +0)
+        auto putk = [&](uint32_t key, float gl) {
+            const float v = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, gl) ^ ((key & 2u) << 30));
+            lds[((key >> 2) & 15u) * stride] = (key & 1u) ? v : 0.f;
+        };
+        putk(ka, g_at1);
+        putk(kb, g_at2);
+        return;
+    }
     auto put = [&](int l, float gl) {
         const float smq = ((posm >> l) & 1u) ? 1.f : (((negm >> l) & 1u) ? -1.f : 0.f);
         lds[l * stride] = (gl * smq) * (((mskm >> l) & 1u) ? 1.f : 0.f);

@@ -70,7 +70,12 @@ def inputs(q):
 def test_qms_code_fast_form(q):
     """The compare-free code (r6) equals the definition on every input, NaN and infinities included."""
     xs = inputs(q)
-    assert np.array_equal(code_definition(xs, q), code_kernel_fast(xs, q))
+    code = code_kernel_fast(xs, q)
+    assert np.array_equal(code_definition(xs, q), code)
+    # the kernel's conversion: fma(code, 1, 1.5 * 2^23) keeps the code in the low mantissa bits; the byte store keeps
+    # the low byte, the code's two's complement
+    byte = ((code + f(12582912.0)).astype(f).view(np.uint32) & 0xFF).astype(np.uint8).view(np.int8)
+    assert np.array_equal(byte.astype(f), code)
 
 
 @pytest.mark.parametrize("q", sorted(HI))
