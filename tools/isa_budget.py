@@ -18,6 +18,7 @@ VALU issue cycles per codeword-iteration are the sum over its four parts' loops.
 SIMD cannot beat whatever the latency hiding, barrier balance or memory system do.
 
 Usage: python tools/isa_budget.py [--func=MANGLED_SUBSTRING --name=KEY --geom=G,P,WPP,THREADS --json=FILE] p0.s p1.s ...
+       python tools/isa_budget.py --func=... --lines=30 p0.s   (r6: the loop's VALU cycles by source line; LINES=1 builds)
 (tools/isa_budget.sh runs it for any generated kernel; the defaults are the cfg3 decode kernel of
 profiles/r4_isa_budget.txt).  r6: any geometry -- the SIMD issue cycles of one workgroup-iteration are the busiest
 SIMD's under round-robin wave placement when one workgroup fills the CU (1024 threads), else the workgroup's total
@@ -116,6 +117,45 @@ def parse(path, func=None):
     return [phases[0] + phases[-1]] + phases[1:-1]
 
 
+def line_costs(path, func, top=30):
+    """(r6, --lines=N) VALU issue cycles of the hot loop by source line, from asm compiled with -gline-tables-only
+    (tools/isa_budget.sh LINES=1): the .loc before each instruction names the innermost inlined source line."""
+    import re
+    text = open(path).read().split("\n")
+    files = {}
+    for ln in text:
+        m = re.match(r'\s*\.file\s+(\d+)\s+"([^"]*)"\s+"([^"]*)"', ln)
+        if m:
+            files[int(m.group(1))] = m.group(3).split("/")[-1]
+    raw, _ = func_lines(path, func)
+    best = None
+    for i, ln in enumerate(raw):
+        if ln.startswith(".LBB") and ln.split(";")[0].strip().endswith(":"):
+            label = ln.split(":")[0]
+            ends = [k for k in range(len(raw) - 1, i, -1) if raw[k].strip().startswith("s_")
+                    and raw[k].strip().split()[-1] == label and "branch" in raw[k]]
+            if ends:
+                nb = sum(1 for k in range(i, ends[0]) if raw[k].strip() == "s_barrier")
+                if best is None or nb > best[0]:
+                    best = (nb, i, ends[0])
+    _, hi, back = best
+    cur, cyc, ops = "?", collections.Counter(), collections.defaultdict(collections.Counter)
+    for ln in raw[hi + 1:back + 1]:
+        t = ln.split(";")[0].strip()
+        m = re.match(r"\.loc\s+(\d+)\s+(\d+)", t)
+        if m:
+            cur = f"{files.get(int(m.group(1)), m.group(1))}:{m.group(2)}"
+            continue
+        if t and not t.startswith(".") and not t.endswith(":") and t.split()[0].startswith("v_"):
+            op = t.split()[0]
+            cyc[cur] += COST[vclass(op)]
+            ops[cur][op] += 1
+    tot = sum(cyc.values())
+    print(f"{path}: {tot:.0f} VALU issue cycles per wave and iteration, by source line")
+    for k, v in cyc.most_common(top):
+        print(f"{v:8.0f} {100 * v / tot:5.1f}%  {k:30s} " + " ".join(f"{o}:{n}" for o, n in ops[k].most_common(4)))
+
+
 def cycles(c):
     return sum(c[k] * COST[k] for k in COST)
 
@@ -191,6 +231,10 @@ if __name__ == "__main__":
     opts = {a.split("=", 1)[0][2:]: a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--")}
     files = [a for a in sys.argv[1:] if not a.startswith("--")]
     geom = tuple(int(v) for v in opts["geom"].split(",")) if "geom" in opts else (1, 8, 2, 1024)
+    if "lines" in opts:
+        for f_ in files:
+            line_costs(f_, opts.get("func"), int(opts["lines"]))
+        sys.exit(0)
     worst = main(files, opts.get("func"), geom)
     if "json" in opts:
         write_json(opts["json"], worst, "tools/isa_budget.sh (gfx950 asm of single-part builds of the library's generator)",
