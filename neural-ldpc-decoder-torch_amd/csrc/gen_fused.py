@@ -25,6 +25,9 @@ import sys
 import numpy as np
 
 PARTS = [int(x) for x in filter(None, os.environ.get("NLDPC_GEN_PARTS", "").split(","))]  # debug
+# graphs whose decode unit also carries the MODE-6 kernels (UCN with CN / UCN / cumulative VN weights: the Boosted
+# NW(1,1,2) decode of the bench's cfg3ucn side lines); the others decode such configurations on MODE 0
+UCNW_TAGS = set(filter(None, os.environ.get("NLDPC_GEN_UCNW", "bg2_z384").split(",")))
 SKIP = set(filter(None, os.environ.get("NLDPC_GEN_SKIP", "").split(",")))  # debug: drop phases
 # diagnostic build only (make STAMPS=1 -> lib_stamps/): s_memtime at every phase boundary of the forward
 # kernels, lane 0 of each wave, first 256 workgroups (FusedArgs::stamps, tools/stamps.py)
@@ -333,7 +336,12 @@ def emit(S: Spec) -> str:
     w("#define CNT (MODE == 2 || MODE == 3)")
     w("#define CM (CNT ? MODE - 1 : 0)  // put_post: store / count / count against y")
     w("#define TIEDW (MODE == 5)")
-    w("#define UCN_ON (!TIEDW && a.ucn)  // (the tied saving forward has no UCN code)")
+    # MODE 6 (r6): MODE 0 specialised for UCN on with CN weights, UCN weights and cumulative VN weights all given -- the
+    # Boosted NW(1,1,2)-like decode: its runtime flags become constants, so their uniform branches and the SGPRs holding
+    # the conditions leave the loop (a part of the MS kernel spilled 110 SGPRs, 48 specialised)
+    w("#define UCNW (MODE == 6)")
+    w("#define UCN_ON (!TIEDW && (UCNW || a.ucn))  // (the tied saving forward has no UCN code)")
+    w("#define WVN_ON (UCNW || a.w_vn != nullptr)")
     w("// check-row LDS addresses from one 32-bit base (ROADDR); in the QMS / SP kernels it measured slower")
     w("#define ROA (KIND == NLDPC_NEURAL || KIND == NLDPC_MS)")
     assert NZ < 65536  # per-codeword error counts are packed two to an LDS word
@@ -456,12 +464,21 @@ def emit(S: Spec) -> str:
                 w("    const bool ucn_ = KIND != NLDPC_NEURAL && UCN_ON;  // UCN: hard decisions of the previous posterior")
             # every posterior's xa (cumulative VN weights) requested before the first posterior store: a later
             # load would wait (vmcnt counts loads and stores in order) for every store issued before it (XPRE)
-            for n, j in enumerate(cols):
-                for i in range(Q):
-                    if "xlreg" in SKIP:  # (fetch bisect, wrong results: the posterior's xa re-read replaced by xin)
-                        w(f"    const float xl_{n}_{i} = xs{i}[{n}];")
-                    else:
-                        w(f"    const float xl_{n}_{i} = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo, {X(j, i)}) : xs{i}[{n}];")
+            # (r6: one branch for the whole group -- a select per load compiled to a branch per load, each reloading the
+            # spilled descriptor's four SGPRs by v_readlane)
+            xls = [(n, j, i) for n, j in enumerate(cols) for i in range(Q)]
+            if "xlreg" in SKIP:  # (fetch bisect, wrong results: the posterior's xa re-read replaced by xin)
+                for n, j, i in xls:
+                    w(f"    const float xl_{n}_{i} = xs{i}[{n}];")
+            elif xls:
+                w("    float " + ", ".join(f"xl_{n}_{i}" for n, j, i in xls) + ";")
+                w("    if (KIND != NLDPC_NEURAL && WVN_ON) {")
+                for n, j, i in xls:
+                    w(f"        xl_{n}_{i} = bload(xr, vo, {X(j, i)});")
+                w("    } else {")
+                for n, j, i in xls:
+                    w(f"        xl_{n}_{i} = xs{i}[{n}];")
+                w("    }")
             s = 0
             for n, j in enumerate(cols):
                 d = len(S.col_edges[j])
@@ -615,15 +632,25 @@ def emit(S: Spec) -> str:
                 # the degree-1 posteriors' channel values (Boosted with cumulative VN weights: from memory) requested
                 # before the row's saved-message stores and check-node work -- a load after a store waits for it
                 # (vmcnt counts both in order): r5, cfg5 training forward 10.8 -> 10.3 ms, cfg3ucn QMS 98.3 -> 95.3 ms
+                d1k = []
                 for k, e in enumerate(es):
                     if e in d1set:
                         j = int(S.hb_cols[e])
                         c, dv = rot(e, q)
                         ix = S.cd_index[p].index((e, q))
-                        if "xld1" in SKIP:  # (fetch bisect, wrong results: the degree-1 posteriors' xa re-read replaced by xin)
-                            w(f"        const float xo{k}_ = cd[{ix}];")
-                        else:
-                            w(f"        const float xo{k}_ = (KIND != NLDPC_NEURAL && a.w_vn) ? bload(xr, vo + {dv}, {4 * (j * Z + c)}) : cd[{ix}];")
+                        d1k.append((k, j, c, dv, ix))
+                if "xld1" in SKIP:  # (fetch bisect, wrong results: the degree-1 posteriors' xa re-read replaced by xin)
+                    for k, j, c, dv, ix in d1k:
+                        w(f"        const float xo{k}_ = cd[{ix}];")
+                elif d1k:  # (one branch for the row copy's loads, as in vn_p)
+                    w("        float " + ", ".join(f"xo{k}_" for k, *_ in d1k) + ";")
+                    w("        if (KIND != NLDPC_NEURAL && WVN_ON) {")
+                    for k, j, c, dv, ix in d1k:
+                        w(f"            xo{k}_ = bload(xr, vo + {dv}, {4 * (j * Z + c)});")
+                    w("        } else {")
+                    for k, j, c, dv, ix in d1k:
+                        w(f"            xo{k}_ = cd[{ix}];")
+                    w("        }")
                 # SAVE: the row copy's v2c, as read, into the saved [E][Z] image by check copy h = u + q*ZT (r5: the
                 # check-node threads store it from their registers; before, the whole workgroup copied each chunk
                 # image between two extra barriers)
@@ -636,7 +663,7 @@ def emit(S: Spec) -> str:
                 w("        }")
                 w(f"        float wv[{DC}], bv[{DC}];")
                 w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{woff[i]} + k]; bv[k] = Bv[{woff[i]} + k]; }}")
-                w("        const bool wc = a.w_cn != nullptr;")
+                w("        const bool wc = UCNW || a.w_cn != nullptr;")
                 w("        float uf_ = 0.f;  // UCN: unsatisfied check (odd number of row variables with APP >= 0)")
                 w("        if (KIND != NLDPC_NEURAL && UCN_ON) {")
                 w("            uint32_t par_ = 0;")
@@ -663,7 +690,7 @@ def emit(S: Spec) -> str:
                 w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
                 w("        }")
                 if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
-                    w(f"        cn_copy<KIND, {DC}, TIEDW>(m{n}, wv, bv, a, wc, {i}, uf_);")
+                    w(f"        cn_copy<KIND, {DC}, TIEDW>(m{n}, wv, bv, a, wc, {i}, uf_, UCN_ON);")
                 for k, e in enumerate(es):
                     if e in d1set:
                         j = int(S.hb_cols[e])
@@ -789,7 +816,7 @@ def emit(S: Spec) -> str:
         def rs(ptr, size):  # descriptor over this block's part of a per-iteration buffer, or an empty one
             return f"make_rsrc({ptr} ? {ptr} + blk * {size} : a.xa, {ptr} ? nlive * {size} : 0)"
 
-        w("    if (KIND != NLDPC_NEURAL && a.w_vn) {  // steps applied before this call's first iteration")
+        w("    if (KIND != NLDPC_NEURAL && WVN_ON) {  // steps applied before this call's first iteration")
         w("        for (int s_ = 0; s_ < a.vn_prefix; ++s_)")
         chan_steps("s_", "            ")
         w("    }")
@@ -807,7 +834,7 @@ def emit(S: Spec) -> str:
         w("    }")
         w("    for (int it = 0; it < a.T; ++it) {")
         stamp(0)
-        w("        if (KIND != NLDPC_NEURAL && a.w_vn) {")
+        w("        if (KIND != NLDPC_NEURAL && WVN_ON) {")
         chan_steps("a.vn_prefix + it", "            ")
         w("            if constexpr (SAVE) {")
         w("                float* sx_ = a.sxin ? a.sxin + it * a.sxin_stride : nullptr;")
@@ -828,7 +855,7 @@ def emit(S: Spec) -> str:
                 w(f"            {bit_set('cdm', ix, app0 + ' >= 0.f')};")
             w("        }")
         # (the check-node threads store the degree-1 columns' xin: cn_p)
-        w("        float* sxd_ = (SAVE && KIND != NLDPC_NEURAL && a.w_vn && a.sxin) ? a.sxin + it * a.sxin_stride : nullptr;")
+        w("        float* sxd_ = (SAVE && KIND != NLDPC_NEURAL && WVN_ON && a.sxin) ? a.sxin + it * a.sxin_stride : nullptr;")
         w(f"        const rsrc_t sxd = make_rsrc(sxd_ ? sxd_ + blk * {NZ} : a.xa, sxd_ ? nlive * {4 * NZ} : 0);")
         w("        const float* pp = it >= 1 ? a.outs.p[it - 1] : nullptr;  // previous iteration's posterior")
         w(f"        const rsrc_t pr = make_rsrc(pp ? pp + blk * {NZ} : a.xa, pp ? nlive * {4 * NZ} : 0);  // no output: stores dropped")
@@ -877,7 +904,7 @@ def emit(S: Spec) -> str:
             if "wload" in SKIP:  # timing experiment only: constant weights, no scalar loads
                 w(f"            for (int k = 0; k < {nw}; ++k) {{ W{ci}[k] = 0.5f; B{ci}[k] = 0.f; }}")
             else:
-                w(f"            if (KIND == NLDPC_NEURAL || wc_) {{ {' '.join(wl)} }}")
+                w(f"            if (KIND == NLDPC_NEURAL || UCNW || wc_) {{ {' '.join(wl)} }}")
                 w(f"            else {{ for (int k = 0; k < {nw}; ++k) W{ci}[k] = 1.f; }}")
                 w(f"            if (KIND == NLDPC_NEURAL || bs_) {{ {' '.join(bl)} }}")
                 w(f"            else {{ for (int k = 0; k < {nw}; ++k) B{ci}[k] = 0.f; }}")
@@ -1008,6 +1035,8 @@ def emit(S: Spec) -> str:
     w("#undef CM")
     w("#undef TIEDW")
     w("#undef UCN_ON")
+    w("#undef UCNW")
+    w("#undef WVN_ON")
     w("}  // namespace")
     return "\n".join(L)
 
@@ -1568,6 +1597,14 @@ def main():
                     src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, {save}>);")
             src.append("    return nullptr;")
             src.append("}")
+            if save == 0:  # (r6) the decode specialised for UCN + CN / UCN / cumulative VN weights, MODE 6, MS / QMS
+                src.append(f"void* fused_{S.tag}_kernel_s0u(int kind) {{")
+                if on and S.tag in UCNW_TAGS:
+                    for k in kinds:
+                        if k in (1, 2):
+                            src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, 6>);")
+                src.append("    return nullptr;")
+                src.append("}")
             if save == 1:  # (r6) the tied saving forward, MODE 5, Boosted MS / QMS
                 src.append(f"void* fused_{S.tag}_kernel_s1t(int kind) {{")
                 if on:
@@ -1611,6 +1648,7 @@ def main():
         src.append(f"void* fused_{S.tag}_bwd(int kind);")
         src.append(f"void* fused_{S.tag}_bwd_tied(int kind);")
         src.append(f"void* fused_{S.tag}_kernel_s1t(int kind);")
+        src.append(f"void* fused_{S.tag}_kernel_s0u(int kind);")
         for v in MODES:
             src.append(f"uint32_t fused_{S.tag}_sig_s{v}();")
         src.append(f"uint32_t fused_{S.tag}_sig_bwd();")
@@ -1624,8 +1662,9 @@ def main():
         kt = ", ".join(f"fused_{S.tag}_bwd_tied({k})" for k in range(4))
         sg = ", ".join([f"fused_{S.tag}_sig_s{v}()" for v in MODES] + [f"fused_{S.tag}_sig_bwd()"] * 2)
         st = ", ".join(f"fused_{S.tag}_kernel_s1t({k})" for k in range(4))
+        su = ", ".join(f"fused_{S.tag}_kernel_s0u({k})" for k in range(4))
         src.append(f"        {{\"{S.tag}\", {S.M}, {S.N}, {S.Z}, {S.E}, {S.G}, {S.threads}, basegraph_{S.tag}, "
-                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}, {{{kt}}}, {{{sg}}}, {{{st}}}}},")
+                   f"{{{ks}}}, {{{kb}}}, {S.lanes_pad // 64}, {{{kt}}}, {{{sg}}}, {{{st}}}, {{{su}}}}},")
     src.append("    };")
     src.append(f"    *n = {len(specs)};")
     src.append("    return tab;")

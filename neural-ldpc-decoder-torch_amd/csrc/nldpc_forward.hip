@@ -297,7 +297,11 @@ static int fused_forward(const nldpc_graph* g, const nldpc_cfg* cfg, int64_t B, 
     // per-edge row in SGPRs (the per-edge kernel spilled ~1 450 SGPRs), the UCN code not compiled
     const bool tied = saved && (cfg->flags & NLDPC_FLAG_CN_TIED) && w_cn && !cfg->ucn &&
                       (cfg->kind == NLDPC_MS || cfg->kind == NLDPC_QMS);
-    const FusedLaunch ft = tied ? fused_launch(g, 6, cfg->kind) : FusedLaunch{};
+    // (r6) a plain decode with UCN and CN / UCN / cumulative VN weights all given (the Boosted NW(1,1,2) decode) runs the
+    // kernel with those flags compiled in when the library has one (MODE 7; fewer uniform branches and SGPR spills)
+    const bool ucnw = mode == 0 && cfg->ucn && w_cn && w_ucn && cfg->vn_cumulative && w_vn &&
+                      (cfg->kind == NLDPC_MS || cfg->kind == NLDPC_QMS);
+    const FusedLaunch ft = tied ? fused_launch(g, 6, cfg->kind) : ucnw ? fused_launch(g, 7, cfg->kind) : FusedLaunch{};
     const FusedLaunch f = ft ? ft : fused_launch(g, mode, cfg->kind);
     if (!f) return fail(NLDPC_EUNSUPPORTED, "no register-resident kernel for this graph / mode / kind");
     FusedArgs fa{};

@@ -655,19 +655,20 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
 // bv: Neural biases, or (Boosted with UCN) the UCN weights; uf: the copy's UCN flag
 // NOUCN: the kernel variant without UCN and with one CN weight per row (the tied saving forward, MODE 5): the UCN
 // branch is not compiled and the row's epilogue is computed once (boosted_row TIED)
+// ucn_on: the kernel's UCN flag (a.ucn, or a constant in the specialised kernels)
 template <int KIND, int DC, bool NOUCN = false>
 __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], const float (&bv)[DC],
-                                        const FusedArgs& a, bool has_w, int row, float uf) {
+                                        const FusedArgs& a, bool has_w, int row, float uf, bool ucn_on) {
     if constexpr (KIND == NLDPC_NEURAL) {
         neural_row<DC>(m, wv, bv);
     } else if constexpr (KIND == NLDPC_MS || KIND == NLDPC_QMS) {
         // QMS reaches the fused kernels only with an active quantiser (fused_eligible): the generic
         // cn_core is not compiled into them (it had made the QMS kernels 6x the code of the MS ones)
-        boosted_row<DC, KIND, NOUCN>(m, wv, has_w, a.qp, a.lo, a.hi, !NOUCN && a.ucn != 0, uf, bv);
+        boosted_row<DC, KIND, NOUCN>(m, wv, has_w, a.qp, a.lo, a.hi, !NOUCN && ucn_on, uf, bv);
     } else {
         CnCore<DC> core;
         cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core, SpRow{a.sp_plan + row * kSpPlanBytes, a.tanh});
-        if (a.ucn) {
+        if (ucn_on) {
 #pragma unroll
             for (int k = 0; k < DC; ++k)
                 m[k] = cn_epilogue<KIND, true>(core.out0[k], wv[k], bv[k], 0.f, uf, has_w, true, a.qbit, a.lo, a.hi).c;
@@ -691,13 +692,15 @@ struct FusedSpec {
                                // fused_launch refuses a kernel whose layout differs from the launcher's
     void* save_tied[4];        // (r6) saving forward for one CN weight per iteration and no UCN (MODE 6 in fused_launch;
                                // the generated kernel<KIND, 5>), or nullptr; built in the saving unit (sig[1])
+    void* decode_ucnw[4];      // (r6) decode with UCN and CN / UCN / cumulative VN weights all given (MODE 7 in
+                               // fused_launch; the generated kernel<KIND, 6>), or nullptr; built in the decode unit (sig[0])
 };
 
 const FusedSpec* fused_specs(int* n);
 
 // How to launch the register-resident kernel of (graph, MODE, kind) (MODE 4: the backward; MODE 5: the
-// backward for tied weights; MODE 6: the saving forward for tied CN weights without UCN -- MODES 5 and 6 library
-// kernels only, a run-time compiled graph uses MODE 4 / 1): one compiled
+// backward for tied weights; MODE 6: the saving forward for tied CN weights without UCN; MODE 7: the decode with UCN
+// and CN / UCN / cumulative VN weights -- MODES 5 to 7 library kernels only, a run-time compiled graph uses MODE 4 / 1): one compiled
 // into the library (fused_specs table, hipLaunchKernel) or one compiled at run time for this graph and
 // attached (nldpc_graph_attach_kernel, hipModuleLaunchKernel); empty when neither exists.
 struct FusedLaunch {

@@ -249,20 +249,22 @@ extern "C" int nldpc_graph_create(int32_t M, int32_t N, int32_t Z, const int32_t
 namespace nldpc {
 FusedLaunch fused_launch(const nldpc_graph* g, int mode, int kind) {
     FusedLaunch L;
-    if (!g || mode < 0 || mode > 6 || kind < 0 || kind > 3) return L;
+    if (!g || mode < 0 || mode > 7 || kind < 0 || kind > 3) return L;
     if (g->fused >= 0) {
         int n = 0;
         const FusedSpec& f = fused_specs(&n)[g->fused];
         // a generated unit built against another argument layout than this launcher (an experiment build
         // mixing objects) would return at once and leave its outputs unwritten: no kernel, the caller reports
         // NLDPC_EUNSUPPORTED for path "fused" or decodes on the streaming kernels
-        const int unit = mode == 6 ? 1 : mode;  // (the tied saving forward lives in the saving unit)
+        // (the tied saving forward lives in the saving unit, the specialised UCN decode in the decode unit)
+        const int unit = mode == 6 ? 1 : mode == 7 ? 0 : mode;
         if (f.sig[unit] != (mode == 4 || mode == 5 ? kFusedBwdArgsSig : kFusedArgsSig)) return L;
-        L.host = mode == 6 ? f.save_tied[kind] : mode == 5 ? f.bwd_tied[kind] : mode == 4 ? f.bwd[kind] : f.kernels[mode][kind];
+        L.host = mode == 7 ? f.decode_ucnw[kind] : mode == 6 ? f.save_tied[kind] : mode == 5 ? f.bwd_tied[kind]
+               : mode == 4 ? f.bwd[kind] : f.kernels[mode][kind];
         L.G = f.G;
         L.threads = f.threads;
         L.waves_per_part = f.waves_per_part;
-    } else if (mode < 5 && g->jit_fn[mode][kind]) {  // (MODES 5 / 6: library kernels only)
+    } else if (mode < 5 && g->jit_fn[mode][kind]) {  // (MODES 5 to 7: library kernels only)
         L.fn = g->jit_fn[mode][kind];
         L.G = g->jit_G;
         L.threads = g->jit_threads;

@@ -28,6 +28,8 @@ VARIANTS = [
      ["fused_bg2_z16_bwd.hip", "fused_bg2_z16_s1.hip"]),
     # (fetch bisect of the training forward, r6: the posteriors' channel re-reads replaced by registers)
     ("skip_xl", {"NLDPC_GEN_SKIP": "xlreg,xld1", "NLDPC_GEN_KINDS": "2", "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z16_s1.hip"]),
+    # (r6: the MODE-6 decode -- UCN with CN / UCN / VN weights compiled in -- for another graph than the default's)
+    ("ucnw_z16", {"NLDPC_GEN_UCNW": "bg2_z16", "NLDPC_GEN_KINDS": "1", "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z16_s0.hip"]),
     # (UREMAT applies to one-codeword geometries: BG2 z=384's training forward; z=16 packs 16 codewords)
     ("uremat_off", {"NLDPC_GEN_UREMAT": "0", "NLDPC_GEN_ONLY": "bg2_z384", "NLDPC_GEN_KINDS": "3",
                     "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z384_s1.hip"]),
@@ -67,5 +69,6 @@ def test_no_pruned_knob_is_read():
     knobs = set(re.findall(r'environ\.get\("(NLDPC_[A-Z_0-9]+)"', src))
     assert knobs <= {"NLDPC_GEN_PARTS", "NLDPC_GEN_SKIP", "NLDPC_GEN_STAMPS", "NLDPC_GEN_GEOM", "NLDPC_GEN_WLATE",
                      "NLDPC_GEN_NOBWD", "NLDPC_GEN_ONLY", "NLDPC_GEN_KINDS", "NLDPC_FUSED_EXTRA", "NLDPC_GEN_UREMAT",
-                     "NLDPC_GEN_BWDPIPE", "NLDPC_GEN_CNBSPARSE", "NLDPC_GEN_BWDCACHE", "NLDPC_GEN_FWDNT8"}, knobs
+                     "NLDPC_GEN_BWDPIPE", "NLDPC_GEN_CNBSPARSE", "NLDPC_GEN_BWDCACHE", "NLDPC_GEN_FWDNT8",
+                     "NLDPC_GEN_UCNW"}, knobs
     assert len(knobs) <= 15

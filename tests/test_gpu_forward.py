@@ -163,6 +163,29 @@ def test_boosted_z384_fused_equals_stream(kind):
     assert torch.equal(res["stream"][1], res["fused"][1])  # final c2v state
 
 
+@pytest.mark.parametrize("kind", [1, 2])
+def test_boosted_z384_ucn_weights_fused_equals_stream(kind):
+    """The decode specialised for UCN with CN / UCN / cumulative VN weights (r6: the library's MODE-7 kernel,
+    kernel<KIND, 6>) against the streaming kernels, bit for bit, at BG2 z=384: per-edge CN and UCN weights, per-column
+    VN weights, and a channel with exact zeros (the punctured columns) for the check node's zero path."""
+    from nldpc.decode import DecodeCfg, decode
+    T, B = 8, 3
+    g = _graph(BG2, 384)
+    gen = torch.Generator().manual_seed(40 + kind)
+    x = (2 * (-1 + 0.9 * torch.randn(B, 52, 384, generator=gen)) / 0.81).float()
+    x[:, :2] = 0.0
+    x = x.to(DEV)
+    w_cn = (0.5 + torch.rand(T, g.E, generator=gen)).to(DEV)
+    w_ucn = (0.3 + torch.rand(T, g.E, generator=gen)).to(DEV)
+    w_vn = (0.8 + 0.4 * torch.rand(T, 52, generator=gen)).to(DEV)
+    res = {}
+    for path in ("stream", "fused"):
+        cfg = DecodeCfg(kind=kind, qbit=5, ucn=True, vn_cumulative=True, path=path)
+        res[path] = decode(g, cfg, x, T, w_cn=w_cn, w_ucn=w_ucn, w_vn=w_vn)
+    assert torch.equal(res["stream"][0], res["fused"][0])
+    assert torch.equal(res["stream"][1], res["fused"][1])  # final c2v state
+
+
 def test_fast_path_selection():
     import ctypes
     from nldpc import _lib

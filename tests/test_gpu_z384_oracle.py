@@ -113,7 +113,7 @@ def test_cfg5_train_step_matches_oracle():
     assert n == 2 * T  # weight_CN_t and weight_VN_t of every iteration
 
 
-@pytest.mark.parametrize("dtype,nw", [(2, (1, 0, 2)), (1, (2, 0, 3)), (2, (3, 3, 0)), (1, (1, 1, 2))])
+@pytest.mark.parametrize("dtype,nw", [(2, (1, 0, 2)), (1, (2, 0, 3)), (2, (3, 3, 0)), (1, (1, 1, 2)), (2, (1, 1, 2))])
 def test_boosted_forward_matches_oracle(dtype, nw):
     """MS / QMS forward at z=384 with random weights: per-edge (code 1), per-check / per-column
     (code 2) and per-iteration (code 3) sharing, UCN weighting (codes 3/3 and 1/1), cumulative VN
