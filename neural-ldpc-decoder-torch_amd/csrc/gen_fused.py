@@ -665,6 +665,7 @@ def emit(S: Spec) -> str:
                 w(f"        for (int k = 0; k < {DC}; ++k) {{ wv[k] = W[{woff[i]} + k]; bv[k] = Bv[{woff[i]} + k]; }}")
                 w("        const bool wc = UCNW || a.w_cn != nullptr;")
                 w("        float uf_ = 0.f;  // UCN: unsatisfied check (odd number of row variables with APP >= 0)")
+                w("        bool ufb_ = false;  // (the same as a lane mask: MS / QMS select on it, SP multiplies by uf_)")
                 w("        if (KIND != NLDPC_NEURAL && UCN_ON) {")
                 w("            uint32_t par_ = 0;")
                 # every word of the row requested first, then the shifts and XORs (one LDS wait, not DC; UCNB)
@@ -687,10 +688,11 @@ def emit(S: Spec) -> str:
                     # (r6: iteration 0's bits -- APP = xa_input or the previous call's posterior -- are set into cdm at
                     # the top of iteration 0, run_p: no per-iteration select between the two sources)
                     w(f"            par_ ^= {bit_get('cdm', ix)};")
-                w("            uf_ = (par_ & 1u) ? 1.f : 0.f;")
+                w("            ufb_ = (par_ & 1u) != 0u;")
+                w("            uf_ = ufb_ ? 1.f : 0.f;")
                 w("        }")
                 if "cnmath" not in SKIP:  # (timing experiment: SKIP=cnmath leaves the messages unchanged)
-                    w(f"        cn_copy<KIND, {DC}, TIEDW>(m{n}, wv, bv, a, wc, {i}, uf_, UCN_ON);")
+                    w(f"        cn_copy<KIND, {DC}, TIEDW>(m{n}, wv, bv, a, wc, {i}, uf_, UCN_ON, ufb_);")
                 for k, e in enumerate(es):
                     if e in d1set:
                         j = int(S.hb_cols[e])

@@ -579,7 +579,7 @@ __device__ __forceinline__ void boosted_row_keys(float (&m)[DC], const float (&w
 #endif
 template <int DC, int KIND, bool TIED = false>
 __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC], bool has_w, const QParams& qp, float lo,
-                                            float hi, bool ucn, float uf, const float (&wu)[DC]) {
+                                            float hi, bool ucn, float uf, const float (&wu)[DC], bool ufb) {
     if constexpr (DC >= 2) {
         float min1, min2;
         if constexpr (DC >= 3) two_smallest_abs3<DC, false>(m, min1, min2);
@@ -631,14 +631,24 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
             }
             // (r6) the weights are 1.f without a CN weight (the kernels' preload), and mag * 1 == mag: no per-edge select of
             // the unweighted value; the UCN weight only with CN weights (the reference's CN sharing 0 ignores UCN)
-            const bool uw = ucn && has_w && uf != 0.f;
+            const bool uw = ucn && has_w && ufb;  // (ufb == (uf != 0): the flag as the lane mask it was computed as)
 #pragma unroll
             for (int k = 0; k < DC; ++k) {
                 const float mag = fabsf(m[k]) == min1 ? mg2 : mg1;
                 // (a wave-uniform branch to the plain weights when no copy is unsatisfied, i.e. two versions
                 // of this loop, measured 15 % slower: code size)
-                const float x1 = NLDPC_TIEDROW ? fmul(mag, uw ? wu[k] : w[k])
-                                               : (!has_w ? mag : fmul(mag, (ucn && uf != 0.f) ? wu[k] : w[k]));
+                float x1;
+                if constexpr (NLDPC_TIEDROW) {
+                    // (r6) both products, then the select: a multiply takes its SGPR weight directly, where a select of
+                    // the two SGPR weights first moved both into VGPRs (two v_mov per edge copy); the fence keeps the
+                    // compiler from folding the select back into the multiply
+                    float xw = fmul(mag, w[k]);
+                    const float xu = fmul(mag, wu[k]);
+                    asm volatile("" : "+v"(xw));
+                    x1 = uw ? xu : xw;
+                } else {
+                    x1 = !has_w ? mag : fmul(mag, (ucn && uf != 0.f) ? wu[k] : w[k]);
+                }
                 float x3;
                 if constexpr (KIND == NLDPC_MS) x3 = __builtin_amdgcn_fmed3f(x1, lo0, top);
                 else x3 = fmul(__builtin_amdgcn_fmed3f(rintf(x1), 0.f, top), inv);
@@ -655,16 +665,16 @@ __device__ __forceinline__ void boosted_row(float (&m)[DC], const float (&w)[DC]
 // bv: Neural biases, or (Boosted with UCN) the UCN weights; uf: the copy's UCN flag
 // NOUCN: the kernel variant without UCN and with one CN weight per row (the tied saving forward, MODE 5): the UCN
 // branch is not compiled and the row's epilogue is computed once (boosted_row TIED)
-// ucn_on: the kernel's UCN flag (a.ucn, or a constant in the specialised kernels)
+// ucn_on: the kernel's UCN flag (a.ucn, or a constant in the specialised kernels); ufb: uf != 0 (uf is 0 or 1)
 template <int KIND, int DC, bool NOUCN = false>
 __device__ __forceinline__ void cn_copy(float (&m)[DC], const float (&wv)[DC], const float (&bv)[DC],
-                                        const FusedArgs& a, bool has_w, int row, float uf, bool ucn_on) {
+                                        const FusedArgs& a, bool has_w, int row, float uf, bool ucn_on, bool ufb) {
     if constexpr (KIND == NLDPC_NEURAL) {
         neural_row<DC>(m, wv, bv);
     } else if constexpr (KIND == NLDPC_MS || KIND == NLDPC_QMS) {
         // QMS reaches the fused kernels only with an active quantiser (fused_eligible): the generic
         // cn_core is not compiled into them (it had made the QMS kernels 6x the code of the MS ones)
-        boosted_row<DC, KIND, NOUCN>(m, wv, has_w, a.qp, a.lo, a.hi, !NOUCN && ucn_on, uf, bv);
+        boosted_row<DC, KIND, NOUCN>(m, wv, has_w, a.qp, a.lo, a.hi, !NOUCN && ucn_on, uf, bv, ufb);
     } else {
         CnCore<DC> core;
         cn_core<DC, KIND>(m, DC, a.qbit, a.lo, a.hi, core, SpRow{a.sp_plan + row * kSpPlanBytes, a.tanh});
