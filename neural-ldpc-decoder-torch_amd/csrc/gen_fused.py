@@ -1556,7 +1556,7 @@ def main():
         print(geo)
         return
     if sys.argv[1] == "--list":  # file names, for the Makefile
-        print(" ".join([f"fused_{t[0]}_s{v}.hip" for t in SPECS for v in MODES] +
+        print(" ".join([f"fused_{t[0]}_s{v}.hip" for t in SPECS for v in MODES] + [f"fused_{t[0]}_s0u.hip" for t in SPECS] +
                        [f"fused_{t[0]}_bwd.hip" for t in SPECS] + ["fused_table.hip"]))
         return
     outdir, res = sys.argv[1], sys.argv[2]
@@ -1599,14 +1599,6 @@ def main():
                     src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, {save}>);")
             src.append("    return nullptr;")
             src.append("}")
-            if save == 0:  # (r6) the decode specialised for UCN + CN / UCN / cumulative VN weights, MODE 6, MS / QMS
-                src.append(f"void* fused_{S.tag}_kernel_s0u(int kind) {{")
-                if on and S.tag in UCNW_TAGS:
-                    for k in kinds:
-                        if k in (1, 2):
-                            src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, 6>);")
-                src.append("    return nullptr;")
-                src.append("}")
             if save == 1:  # (r6) the tied saving forward, MODE 5, Boosted MS / QMS
                 src.append(f"void* fused_{S.tag}_kernel_s1t(int kind) {{")
                 if on:
@@ -1617,6 +1609,21 @@ def main():
                 src.append("}")
             src.append("}  // namespace nldpc")
             write(f"fused_{S.tag}_s{save}.hip", src)
+        # (r6) the decode specialised for UCN + CN / UCN / cumulative VN weights, MODE 6, MS / QMS: a unit of its own, so its
+        # code object holds these two kernels only (the same kernel code placed after the generic decode kernels of
+        # every kind ran 1.3 % slower, profiles/r6_ab_ucn_select.txt: instruction-cache placement)
+        src = list(head)
+        ucnw = on and S.tag in UCNW_TAGS and any(k in (1, 2) for k in kinds)
+        src.append(body if ucnw else "")
+        src.append(f"void* fused_{S.tag}_kernel_s0u(int kind) {{")
+        if ucnw:
+            for k in kinds:
+                if k in (1, 2):
+                    src.append(f"    if (kind == {k}) return reinterpret_cast<void*>(&fused_{S.tag}::kernel<{k}, 6>);")
+        src.append("    return nullptr;")
+        src.append("}")
+        src.append("}  // namespace nldpc")
+        write(f"fused_{S.tag}_s0u.hip", src)
         # backward kernels: the fp32-message kinds and QMS (int8 codes) stage their saved messages in LDS
         # beside chunk images sized for them, so they are two generated namespaces
         src = list(head)

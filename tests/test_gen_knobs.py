@@ -29,7 +29,7 @@ VARIANTS = [
     # (fetch bisect of the training forward, r6: the posteriors' channel re-reads replaced by registers)
     ("skip_xl", {"NLDPC_GEN_SKIP": "xlreg,xld1", "NLDPC_GEN_KINDS": "2", "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z16_s1.hip"]),
     # (r6: the MODE-6 decode -- UCN with CN / UCN / VN weights compiled in -- for another graph than the default's)
-    ("ucnw_z16", {"NLDPC_GEN_UCNW": "bg2_z16", "NLDPC_GEN_KINDS": "1", "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z16_s0.hip"]),
+    ("ucnw_z16", {"NLDPC_GEN_UCNW": "bg2_z16", "NLDPC_GEN_KINDS": "1", "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z16_s0u.hip"]),
     # (UREMAT applies to one-codeword geometries: BG2 z=384's training forward; z=16 packs 16 codewords)
     ("uremat_off", {"NLDPC_GEN_UREMAT": "0", "NLDPC_GEN_ONLY": "bg2_z384", "NLDPC_GEN_KINDS": "3",
                     "NLDPC_GEN_NOBWD": "1"}, ["fused_bg2_z384_s1.hip"]),
